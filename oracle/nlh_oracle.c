@@ -1,0 +1,263 @@
+/*
+ * nlh_oracle.c -- CPU ORACLE (test infrastructure only; see nlh_oracle.h).
+ *
+ * Plain-C restatement of the reference serial solver
+ *   /root/reference/src/2d_nonlocal_serial.cpp
+ * with the per-term floating-point operation order kept exactly:
+ *   sum_local       :256-270   res += ((1.0*c_2d)*(u_j - u_i))*(dh*dh)
+ *   sum_local_test  :235-252   res  = -(((2pi*sin(2pi*(t*dt)))*sin(2pi*(x*dh)))*sin(2pi*(y*dh)))
+ *                              res -= ((1.0*c_2d)*(w~_j - w_i))*(dh*dh)
+ *   w               :207-210   (cos(2pi*(t*dt))*sin(2pi*(x*dh)))*sin(2pi*(y*dh))
+ *   boundary        :213-221   0 outside [0,nx)x[0,ny)
+ *   len_1d_line     :231       (long)sqrt(eps*eps - dx*dx)
+ *   do_work         :273-303   u' = u + sum_local*dt ; u' += sum_local_test*dt
+ *   compute_l2/linf :96-113    sx-outer, sy-inner accumulation
+ * Build with -ffp-contract=off (the reference is built without -march, so
+ * x86-64 never contracts a*b+c into an FMA; CMakeLists.txt:23).
+ *
+ * sin(2pi*(x*dh)) is a pure function of x, so it is tabulated once per run;
+ * the values are the same doubles the reference recomputes per neighbour.
+ */
+#define _GNU_SOURCE
+#include "nlh_oracle.h"
+
+#include <math.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#ifndef M_PI
+#define M_PI 3.14159265358979323846
+#endif
+
+double nlh_oracle_c2d(const nlh_oracle_params *p) {
+  return (p->k * 8) / pow(p->eps * p->dh, 4);
+}
+
+static long line_len(long eps, long dx) {
+  return (long)sqrt((double)((eps * eps) - (dx * dx)));
+}
+
+long nlh_oracle_disk_count(long eps) {
+  long n = 0;
+  for (long dx = -eps; dx <= eps; ++dx) n += 2 * line_len(eps, labs(dx)) + 1;
+  return n;
+}
+
+/* sin(2*pi*(i*dh)) for i in [lo, hi) -- the factor of w and of the IC */
+static double *sin_table(long lo, long hi, double dh) {
+  double *t = (double *)malloc(sizeof(double) * (size_t)(hi - lo));
+  for (long i = lo; i < hi; ++i) t[i - lo] = sin(2 * M_PI * (i * dh));
+  return t;
+}
+
+void nlh_oracle_test_init(const nlh_oracle_params *p, double *u) {
+  for (long sx = 0; sx < p->nx; ++sx)
+    for (long sy = 0; sy < p->ny; ++sy)
+      u[sx + sy * p->nx] = sin(2 * M_PI * (sx * p->dh)) * sin(2 * M_PI * (sy * p->dh));
+}
+
+void nlh_oracle_exact(const nlh_oracle_params *p, long t, double *w) {
+  const double ct = cos(2 * M_PI * (t * p->dt));
+  for (long sx = 0; sx < p->nx; ++sx)
+    for (long sy = 0; sy < p->ny; ++sy)
+      w[sx + sy * p->nx] = ct * sin(2 * M_PI * (sx * p->dh)) * sin(2 * M_PI * (sy * p->dh));
+}
+
+/* ------------------------------------------------------------------------- */
+typedef struct {
+  const nlh_oracle_params *p;
+  double c2d, dh2, st, ct;
+  const double *sx_tab; /* index x + eps, covers [-eps, nx+eps) */
+  const double *sy_tab; /* index y + eps, covers [-eps, ny+eps) */
+} step_ctx;
+
+/* sum_local (:256-270) */
+static double sum_local(const step_ctx *c, const double *u, long x, long y) {
+  const long nx = c->p->nx, ny = c->p->ny, eps = c->p->eps;
+  const double ui = u[x + y * nx];
+  double res = 0.0;
+  for (long sx = x - eps; sx <= x + eps; ++sx) {
+    const long len = line_len(eps, labs(x - sx));
+    const int inx = (sx >= 0 && sx < nx);
+    for (long sy = y - len; sy <= y + len; ++sy) {
+      const double v = (inx && sy >= 0 && sy < ny) ? u[sx + sy * nx] : 0.0;
+      res += ((1.0 * c->c2d) * (v - ui)) * c->dh2;
+    }
+  }
+  return res;
+}
+
+/* sum_local_test (:235-252), w via the tabulated sin factors */
+static double sum_local_test(const step_ctx *c, long x, long y) {
+  const long nx = c->p->nx, ny = c->p->ny, eps = c->p->eps;
+  const double sxv = c->sx_tab[x + eps], syv = c->sy_tab[y + eps];
+  double res = -(((2 * M_PI) * c->st) * sxv * syv);
+  const double wpos = c->ct * sxv * syv;
+  for (long sx = x - eps; sx <= x + eps; ++sx) {
+    const long len = line_len(eps, labs(x - sx));
+    const int inx = (sx >= 0 && sx < nx);
+    for (long sy = y - len; sy <= y + len; ++sy) {
+      const double wv =
+          (inx && sy >= 0 && sy < ny) ? c->ct * c->sx_tab[sx + eps] * c->sy_tab[sy + eps] : 0.0;
+      res -= ((1.0 * c->c2d) * (wv - wpos)) * c->dh2;
+    }
+  }
+  return res;
+}
+
+static void step_rect(const step_ctx *c, const double *u, double *un, long x0,
+                      long x1, long y0, long y1) {
+  const long nx = c->p->nx;
+  const double dt = c->p->dt;
+  for (long y = y0; y < y1; ++y)
+    for (long x = x0; x < x1; ++x) {
+      const long i = x + y * nx;
+      un[i] = u[i] + (sum_local(c, u, x, y) * dt);
+      if (c->p->test) un[i] += sum_local_test(c, x, y) * dt;
+    }
+}
+
+static void ctx_init(step_ctx *c, const nlh_oracle_params *p) {
+  c->p = p;
+  c->c2d = nlh_oracle_c2d(p);
+  c->dh2 = p->dh * p->dh;
+  c->sx_tab = sin_table(-p->eps, p->nx + p->eps, p->dh);
+  c->sy_tab = sin_table(-p->eps, p->ny + p->eps, p->dh);
+}
+
+static void ctx_time(step_ctx *c, long t) {
+  c->st = sin(2 * M_PI * (t * c->p->dt));
+  c->ct = cos(2 * M_PI * (t * c->p->dt));
+}
+
+static void ctx_free(step_ctx *c) {
+  free((void *)c->sx_tab);
+  free((void *)c->sy_tab);
+}
+
+/* ------------------------------------------------------------------------- */
+/* persistent worker pool: tiles pulled from a shared counter, barrier/step   */
+typedef struct {
+  step_ctx *c;
+  const double *u;
+  double *un;
+  long tiles_x, tiles_y, tw, th;
+  long next_tile;
+  pthread_mutex_t mu;
+} tile_job;
+
+static void *tile_worker(void *arg) {
+  tile_job *j = (tile_job *)arg;
+  const long ntiles = j->tiles_x * j->tiles_y;
+  for (;;) {
+    pthread_mutex_lock(&j->mu);
+    const long t = j->next_tile++;
+    pthread_mutex_unlock(&j->mu);
+    if (t >= ntiles) break;
+    const long gx = t % j->tiles_x, gy = t / j->tiles_x;
+    const long x0 = gx * j->tw, y0 = gy * j->th;
+    long x1 = x0 + j->tw, y1 = y0 + j->th;
+    if (x1 > j->c->p->nx) x1 = j->c->p->nx;
+    if (y1 > j->c->p->ny) y1 = j->c->p->ny;
+    step_rect(j->c, j->u, j->un, x0, x1, y0, y1);
+  }
+  return NULL;
+}
+
+static void run_tiles(step_ctx *c, const double *u, double *un, long tiles_x,
+                      long tiles_y, int nthreads) {
+  tile_job j;
+  j.c = c;
+  j.u = u;
+  j.un = un;
+  j.tiles_x = tiles_x;
+  j.tiles_y = tiles_y;
+  j.tw = (c->p->nx + tiles_x - 1) / tiles_x;
+  j.th = (c->p->ny + tiles_y - 1) / tiles_y;
+  j.next_tile = 0;
+  pthread_mutex_init(&j.mu, NULL);
+  if (nthreads <= 1) {
+    tile_worker(&j);
+  } else {
+    pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)nthreads);
+    for (int i = 0; i < nthreads; ++i) pthread_create(&th[i], NULL, tile_worker, &j);
+    for (int i = 0; i < nthreads; ++i) pthread_join(th[i], NULL); /* = barrier */
+    free(th);
+  }
+  pthread_mutex_destroy(&j.mu);
+}
+
+void nlh_oracle_step(const nlh_oracle_params *p, long t, const double *u,
+                     double *un, int nthreads) {
+  step_ctx c;
+  ctx_init(&c, p);
+  ctx_time(&c, t);
+  long rows = nthreads > 1 ? 4L * nthreads : 1;
+  if (rows > p->ny) rows = p->ny > 0 ? p->ny : 1;
+  run_tiles(&c, u, un, 1, rows, nthreads);
+  ctx_free(&c);
+}
+
+void nlh_oracle_run(const nlh_oracle_params *p, long nt, double *u,
+                    int nthreads) {
+  const size_t n = (size_t)(p->nx * p->ny);
+  double *b = (double *)malloc(sizeof(double) * (n ? n : 1));
+  step_ctx c;
+  ctx_init(&c, p);
+  double *cur = u, *nxt = b;
+  long rows = nthreads > 1 ? 4L * nthreads : 1;
+  if (rows > p->ny) rows = p->ny > 0 ? p->ny : 1;
+  for (long t = 0; t < nt; ++t) {
+    ctx_time(&c, t);
+    run_tiles(&c, cur, nxt, 1, rows, nthreads);
+    double *tmp = cur;
+    cur = nxt;
+    nxt = tmp;
+  }
+  if (cur != u) memcpy(u, cur, sizeof(double) * n);
+  ctx_free(&c);
+  free(b);
+}
+
+void nlh_oracle_errors(const nlh_oracle_params *p, long time, const double *u,
+                       double *l2, double *linf) {
+  const double ct = cos(2 * M_PI * (time * p->dt));
+  double e2 = 0, ei = 0;
+  for (long sx = 0; sx < p->nx; ++sx) {
+    const double sxv = sin(2 * M_PI * (sx * p->dh));
+    for (long sy = 0; sy < p->ny; ++sy) {
+      const double w = ct * sxv * sin(2 * M_PI * (sy * p->dh));
+      const double d = u[sx + sy * p->nx] - w;
+      e2 += d * d;
+      const double a = fabs(d);
+      ei = (a < ei) ? ei : a; /* std::max(abs(..), error_linf) */
+    }
+  }
+  *l2 = e2;
+  *linf = ei;
+}
+
+double nlh_oracle_run_tiled(const nlh_oracle_params *p, long nt, long tiles_x,
+                            long tiles_y, double *u, int nthreads) {
+  const size_t n = (size_t)(p->nx * p->ny);
+  double *b = (double *)malloc(sizeof(double) * (n ? n : 1));
+  step_ctx c;
+  ctx_init(&c, p);
+  double *cur = u, *nxt = b;
+  struct timespec t0, t1;
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+  for (long t = 0; t < nt; ++t) {
+    ctx_time(&c, t);
+    run_tiles(&c, cur, nxt, tiles_x, tiles_y, nthreads);
+    double *tmp = cur;
+    cur = nxt;
+    nxt = tmp;
+  }
+  clock_gettime(CLOCK_MONOTONIC, &t1);
+  if (cur != u) memcpy(u, cur, sizeof(double) * n);
+  ctx_free(&c);
+  free(b);
+  return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}

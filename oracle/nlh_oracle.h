@@ -1,0 +1,71 @@
+/*
+ * nlh_oracle.h -- CPU ORACLE (test infrastructure only).
+ *
+ * A plain-C restatement of the reference's 2D nonlocal heat-equation solver
+ * (src/2d_nonlocal_serial.cpp in nonlocalmodels/nonlocalheatequation).  It is
+ * the CHECKER for the HIP path: only tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py may load it.  The product library (libnlh.so)
+ * never links or calls it.
+ *
+ * Parity pinning: the restatement reproduces, bit for bit, the known answers
+ * recorded in SURVEY.md Appendix A (full-precision l2 / linf / sum / u[1+nx]
+ * produced by the survey's probe of the unmodified reference serial solver)
+ * and passes the reference's own batch contract (tests/2d*.txt, error_l2/N <=
+ * 1e-6, CMakeLists.txt:116-154).  See tests/test_oracle.py.
+ */
+#ifndef NLH_ORACLE_H
+#define NLH_ORACLE_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct {
+  long nx, ny;   /* global lattice size (x fastest, index x + y*nx)        */
+  long eps;      /* horizon in lattice cells                               */
+  double k;      /* heat transfer coefficient                              */
+  double dt;     /* time step                                              */
+  double dh;     /* lattice spacing                                        */
+  int test;      /* 1: add manufactured source (sum_local_test)            */
+} nlh_oracle_params;
+
+/* c_2d = (k*8)/pow(eps*dh,4)   -- src/2d_nonlocal_serial.cpp:76 */
+double nlh_oracle_c2d(const nlh_oracle_params *p);
+
+/* number of lattice points in the closed disk dx^2+dy^2 <= eps^2, counted the
+ * way the reference loops (len_1d_line truncation, :231,260-262)            */
+long nlh_oracle_disk_count(long eps);
+
+/* IC of test_init(): sin(2*pi*(x*dh))*sin(2*pi*(y*dh))  (:190-198)          */
+void nlh_oracle_test_init(const nlh_oracle_params *p, double *u);
+
+/* exact solution w(x,y,t) (:207-210) into a full field                      */
+void nlh_oracle_exact(const nlh_oracle_params *p, long t, double *w);
+
+/* One explicit-Euler step t: un = u + sum_local*dt (+ sum_local_test*dt)
+ * (:279-284).  Nodes are partitioned over `nthreads` pthreads (Jacobi update,
+ * so the result does not depend on the partition).                          */
+void nlh_oracle_step(const nlh_oracle_params *p, long t, const double *u,
+                     double *un, int nthreads);
+
+/* nt steps starting from u (overwritten with the state at time nt).        */
+void nlh_oracle_run(const nlh_oracle_params *p, long nt, double *u,
+                    int nthreads);
+
+/* compute_l2 / compute_linf at `time` (:96-113): l2 = sum (u-w)^2 accumulated
+ * sx-outer / sy-inner, no sqrt;  linf = max |u-w|                           */
+void nlh_oracle_errors(const nlh_oracle_params *p, long time, const double *u,
+                       double *l2, double *linf);
+
+/* Tiled CPU baseline: restatement of 2d_nonlocal_async's execution model
+ * (src/2d_nonlocal_async.cpp:382-473): np_x*np_y tiles, one task per tile per
+ * step pulled from a shared counter by `nthreads` workers, one barrier per
+ * step.  Same per-node arithmetic as the serial oracle, so bitwise identical
+ * results.  Returns the wall time in seconds of the nt-step loop.           */
+double nlh_oracle_run_tiled(const nlh_oracle_params *p, long nt, long tiles_x,
+                            long tiles_y, double *u, int nthreads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
