@@ -1,0 +1,59 @@
+# Build of the MI355X-native nonlocal heat-equation solver.
+#   libnlh.so   C-ABI solver library (HIP kernels for gfx950 + RCCL)
+#   bin/2d_nonlocal_{serial,async,distributed}   drop-in CLI drivers
+#   oracle/liboracle.so   CPU checker (test infrastructure only)
+ROCM    ?= /opt/rocm
+HIPCC   ?= $(ROCM)/bin/hipcc
+ARCH    ?= gfx950
+PKG     := nonlocalheatequation_amd
+CSRC    := $(PKG)/csrc
+LIBDIR  := $(PKG)/lib
+OBJDIR  := build/obj
+BINDIR  := bin
+
+CXXSTD  := -std=c++17
+WARN    := -Wall -Wextra -Wno-unused-parameter
+INC     := -Iinclude -I$(CSRC)
+HIPFLAGS := --offload-arch=$(ARCH) -O3 $(CXXSTD) -fPIC $(WARN) $(INC) -munsafe-fp-atomics
+HOSTFLAGS := -O2 $(CXXSTD) -fPIC $(WARN) $(INC) -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include
+
+LIB_OBJS := $(OBJDIR)/nlh_kernels.o $(OBJDIR)/nlh_api.o $(OBJDIR)/nlh_plan.o
+DRIVERS  := $(BINDIR)/2d_nonlocal_serial $(BINDIR)/2d_nonlocal_async $(BINDIR)/2d_nonlocal_distributed
+DRV_COMMON := $(OBJDIR)/driver_common.o $(OBJDIR)/vtu_writer.o
+
+all: lib drivers oracle
+lib: $(LIBDIR)/libnlh.so
+drivers: $(DRIVERS)
+oracle:
+	$(MAKE) -s -C oracle
+
+$(OBJDIR) $(LIBDIR) $(BINDIR):
+	mkdir -p $@
+
+$(OBJDIR)/nlh_kernels.o: $(CSRC)/nlh_kernels.hip $(CSRC)/nlh_device.h | $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OBJDIR)/nlh_api.o: $(CSRC)/nlh_api.cpp $(CSRC)/nlh_device.h $(CSRC)/nlh_plan.h include/nlh.h | $(OBJDIR)
+	$(HIPCC) $(HOSTFLAGS) -x c++ -c $< -o $@
+
+$(OBJDIR)/nlh_plan.o: $(CSRC)/nlh_plan.cpp $(CSRC)/nlh_plan.h | $(OBJDIR)
+	g++ $(HOSTFLAGS) -c $< -o $@
+
+$(LIBDIR)/libnlh.so: $(LIB_OBJS) | $(LIBDIR)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(LIB_OBJS) -L$(ROCM)/lib -lrccl -Wl,-rpath,$(ROCM)/lib
+
+$(OBJDIR)/driver_common.o: $(CSRC)/drivers/driver_common.cpp $(CSRC)/drivers/driver_common.h include/nlh.h | $(OBJDIR)
+	g++ -O2 $(CXXSTD) $(WARN) $(INC) -c $< -o $@
+
+$(OBJDIR)/vtu_writer.o: $(CSRC)/drivers/vtu_writer.cpp $(CSRC)/drivers/vtu_writer.h | $(OBJDIR)
+	g++ -O2 $(CXXSTD) $(WARN) $(INC) -c $< -o $@
+
+$(BINDIR)/%: $(CSRC)/drivers/%.cpp $(DRV_COMMON) $(LIBDIR)/libnlh.so | $(BINDIR)
+	g++ -O2 $(CXXSTD) $(WARN) $(INC) $< $(DRV_COMMON) -o $@ -L$(LIBDIR) -lnlh \
+	    -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)' -Wl,-rpath,$(ROCM)/lib -lpthread
+
+clean:
+	rm -rf build $(LIBDIR) $(BINDIR)
+	$(MAKE) -s -C oracle clean
+
+.PHONY: all lib drivers oracle clean

@@ -1,0 +1,150 @@
+/*
+ * nlh.h -- C ABI of libnlh, the MI355X-native solver for the explicit-Euler
+ * hot path of the 2D nonlocal heat equation (nonlocalmodels/
+ * nonlocalheatequation).  Plain C types only; no HIP, RCCL or torch types in
+ * any signature.
+ *
+ * The reference has no plugin/FFI layer: its hot path is a member of the
+ * `solver` class compiled into each executable.  Every entry point below
+ * replaces one piece of that class (citations are /root/reference paths):
+ *
+ *   nlh_create        solver::solver(...)                src/2d_nonlocal_serial.cpp:70-93
+ *                     (c_2d :76; tile grid/ownership     src/2d_nonlocal_async.cpp:131-164,
+ *                      locidx / --file map)              src/2d_nonlocal_distributed.cpp:105-110,415-488)
+ *   nlh_init_test     solver::test_init()                src/2d_nonlocal_serial.cpp:190-198
+ *                     partition_space(nx,ny,gx,gy)       src/2d_nonlocal_async.cpp:70-78
+ *   nlh_set_field     solver::input_init()               src/2d_nonlocal_serial.cpp:180-187
+ *   nlh_run           solver::do_work() time loop        src/2d_nonlocal_serial.cpp:273-303
+ *                     (sum_local :256-270, sum_local_test :235-252, boundary :213-221)
+ *                     sum_local_partition per tile       src/2d_nonlocal_async.cpp:382-404,
+ *                                                        src/2d_nonlocal_distributed.cpp:1146-1262
+ *   nlh_get_field     S[nt % 2] returned by do_work      src/2d_nonlocal_serial.cpp:302
+ *   nlh_errors        compute_l2 / compute_linf          src/2d_nonlocal_serial.cpp:96-113
+ *                                                        src/2d_nonlocal_distributed.cpp:495-520
+ *   nlh_destroy       ~solver
+ *
+ * Conventions
+ *   - Fields cross the boundary as GLOBAL host arrays of nx*ny doubles with
+ *     the reference's index x + y*nx (x fastest).  Each rank reads/writes only
+ *     the nodes it owns; host memory is caller-owned.
+ *   - The library owns all device memory and its HIP streams.  One handle per
+ *     host thread.  Calls are synchronous unless stated otherwise.
+ *   - Every function returns NLH_OK (0) or an error code; nlh_last_error()
+ *     returns a thread-local message for the last failure.  There is no CPU
+ *     fallback: without a usable gfx950 device nlh_create fails loudly.
+ */
+#ifndef NLH_H
+#define NLH_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NLH_ABI_VERSION 1
+
+enum nlh_status {
+  NLH_OK = 0,
+  NLH_ERR_ARG = 1,         /* invalid parameter                          */
+  NLH_ERR_HIP = 2,         /* HIP runtime failure                        */
+  NLH_ERR_RCCL = 3,        /* RCCL failure                               */
+  NLH_ERR_STATE = 4,       /* call not valid in the current state        */
+  NLH_ERR_UNSUPPORTED = 5  /* configuration not supported               */
+};
+
+/* Stencil implementation.  EXACT reproduces the reference's per-term
+ * floating-point order bit for bit (4 ops per neighbour).  FAST computes the
+ * same J=1 disk sum by nested row windows (~4*eps adds per node, HBM-bound);
+ * it differs from the reference only by summation rounding.  AUTO = EXACT
+ * when the manufactured source is on (test=1, where the L2 error is the
+ * output), FAST otherwise (production runs).                             */
+enum nlh_kernel { NLH_KERNEL_AUTO = 0, NLH_KERNEL_EXACT = 1, NLH_KERNEL_FAST = 2 };
+
+typedef struct nlh_params {
+  int64_t nx, ny;       /* global lattice size in nodes                        */
+  int64_t eps;          /* horizon in lattice cells (>= 1)                     */
+  double k, dt, dh;     /* heat coefficient, time step, lattice spacing        */
+  int32_t test;         /* 1: add the manufactured-solution source             */
+  int32_t kernel;       /* enum nlh_kernel                                     */
+  int32_t device;       /* HIP device ordinal, -1 = current device             */
+  int32_t rank;         /* this process, 0 <= rank < nranks                    */
+  int32_t nranks;       /* processes (one per GPU); 1 = single GPU             */
+  int32_t seg_rows;     /* FAST kernel segment height, 0 = automatic           */
+  int64_t tiles_x;      /* tile grid over the lattice (reference npx / np);    */
+  int64_t tiles_y;      /*   must divide nx / ny.  1x1 for the serial driver   */
+  const int32_t *owner; /* tiles_x*tiles_y owner ranks, index gx + gy*tiles_x; */
+                        /*   NULL = reference default locidx(): i*nranks/T     */
+  const uint8_t *comm_id; /* NLH_COMM_ID_BYTES RCCL unique id (nranks > 1)     */
+} nlh_params;
+
+typedef struct nlh_solver nlh_solver;
+
+#define NLH_COMM_ID_BYTES 128
+
+/* Fill `id` with a fresh RCCL unique id (rank 0), to be broadcast to every
+ * rank out of band (e.g. torch.distributed) before nlh_create.             */
+int nlh_comm_unique_id(uint8_t id[NLH_COMM_ID_BYTES]);
+
+int nlh_create(const nlh_params *p, nlh_solver **out);
+int nlh_destroy(nlh_solver *s);
+
+/* test_init(): u(x,y,0) = sin(2*pi*(x*dh))*sin(2*pi*(y*dh)); step := 0.   */
+int nlh_init_test(nlh_solver *s);
+/* input_init(): global host field (x + y*nx); step := 0.                  */
+int nlh_set_field(nlh_solver *s, const double *u_global);
+/* Copy the owned nodes of the current field into the global host array.   */
+int nlh_get_field(nlh_solver *s, double *u_global);
+
+/* Advance `nsteps` explicit-Euler steps from the current step index.
+ * Asynchronous: returns once the work is enqueued (nlh_synchronize waits). */
+int nlh_run(nlh_solver *s, int64_t nsteps);
+int nlh_synchronize(nlh_solver *s);
+/* Current step index t (the field holds u(t)).                            */
+int64_t nlh_step_index(const nlh_solver *s);
+
+/* error_l2 = sum (u - w(time))^2 (no sqrt, as the reference), error_linf =
+ * max |u - w(time)| over the GLOBAL lattice (all-reduced over ranks).     */
+int nlh_errors(nlh_solver *s, int64_t time, double *l2, double *linf);
+
+/* Introspection for tests / benchmarks. */
+typedef struct nlh_info {
+  int32_t kernel;          /* resolved enum nlh_kernel                     */
+  int32_t device;          /* HIP device ordinal in use                    */
+  int32_t nblocks;         /* owned rectangular blocks on this rank        */
+  int32_t npeers;          /* ranks exchanged with each step               */
+  int64_t owned_nodes;     /* nodes owned by this rank                     */
+  int64_t disk_points;     /* N(eps): lattice points in the closed disk    */
+  int64_t halo_bytes_sent; /* bytes sent per step to other ranks          */
+  int64_t device_bytes;    /* device memory held by the solver             */
+  char    arch[32];        /* gcnArchName of the device                    */
+} nlh_info;
+int nlh_get_info(const nlh_solver *s, nlh_info *info);
+
+/* Stencil-kernel timing with HIP events recorded on the stream the stencil
+ * kernels are launched on.  While enabled, every stencil launch of nlh_run
+ * is bracketed by events; nlh_kernel_time returns the summed duration and the
+ * launch count since the last enable.                                      */
+int nlh_kernel_timing(nlh_solver *s, int enable);
+int nlh_kernel_time(nlh_solver *s, double *total_ms, int64_t *launches);
+
+/* Host-only (no device work): the owner rank of each tile as resolved by the
+ * library (reference locidx(), src/2d_nonlocal_distributed.cpp:105-110).  */
+int nlh_resolve_owner(int64_t tiles_x, int64_t tiles_y, int32_t nranks,
+                      const int32_t *owner_in, int32_t *owner_out);
+
+/* Host-only halo plan, for tests of the decomposition: number of halo
+ * pieces this rank receives per step and, if `pieces` is non-NULL, up to
+ * `cap` records of 8 int64 each:
+ *   {src_rank, dst_rank, gx0, gy0, w, h, src_block, dst_block}
+ * (a global rectangle copied from the owner's interior into the halo of
+ * block dst_block of dst_rank).                                           */
+int64_t nlh_halo_plan(const nlh_params *p, int64_t *pieces, int64_t cap);
+
+const char *nlh_last_error(void);
+int nlh_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NLH_H */

@@ -1,0 +1,357 @@
+"""nonlocalheatequation_amd -- MI355X-native solver for the explicit-Euler hot
+path of the 2D nonlocal heat equation (nonlocalmodels/nonlocalheatequation).
+
+This module is the Python host mirror of the reference's ``solver`` class
+(/root/reference/src/2d_nonlocal_serial.cpp:31-304) over the C ABI of
+``lib/libnlh.so`` (include/nlh.h).  All numerics run in the gfx950 HIP
+kernels of that library; there is no CPU fallback -- constructing a
+:class:`Solver` without the built library or without a GPU raises.
+
+Reference correspondences::
+
+    Solver(...)              solver::solver(nx, ny, nt, eps, nlog)     :70-93
+    Solver.test_init()       solver::test_init()                        :190-198
+    Solver.input_init(u)     solver::input_init()                       :180-187
+    Solver.do_work(nt)       solver::do_work()                          :273-303
+    Solver.compute_l2(t)     solver::compute_l2(time)                   :96-103
+    Solver.compute_linf(t)   solver::compute_linf(time)                 :106-113
+    batch_tester(text)       batch_tester()                             :306-333
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+__all__ = [
+    "KERNEL_AUTO", "KERNEL_EXACT", "KERNEL_FAST", "NLHError", "Solver",
+    "lib", "lib_path", "comm_unique_id", "resolve_owner", "halo_plan",
+    "disk_count", "batch_tester", "BatchRow",
+]
+
+KERNEL_AUTO, KERNEL_EXACT, KERNEL_FAST = 0, 1, 2
+_KERNEL_NAMES = {"auto": KERNEL_AUTO, "exact": KERNEL_EXACT, "fast": KERNEL_FAST}
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def lib_path() -> str:
+    return os.path.join(_HERE, "lib", "libnlh.so")
+
+
+class NLHError(RuntimeError):
+    pass
+
+
+class _Params(ctypes.Structure):
+    _fields_ = [
+        ("nx", ctypes.c_int64), ("ny", ctypes.c_int64), ("eps", ctypes.c_int64),
+        ("k", ctypes.c_double), ("dt", ctypes.c_double), ("dh", ctypes.c_double),
+        ("test", ctypes.c_int32), ("kernel", ctypes.c_int32), ("device", ctypes.c_int32),
+        ("rank", ctypes.c_int32), ("nranks", ctypes.c_int32), ("seg_rows", ctypes.c_int32),
+        ("tiles_x", ctypes.c_int64), ("tiles_y", ctypes.c_int64),
+        ("owner", ctypes.POINTER(ctypes.c_int32)),
+        ("comm_id", ctypes.POINTER(ctypes.c_uint8)),
+    ]
+
+
+class _Info(ctypes.Structure):
+    _fields_ = [
+        ("kernel", ctypes.c_int32), ("device", ctypes.c_int32), ("nblocks", ctypes.c_int32),
+        ("npeers", ctypes.c_int32), ("owned_nodes", ctypes.c_int64), ("disk_points", ctypes.c_int64),
+        ("halo_bytes_sent", ctypes.c_int64), ("device_bytes", ctypes.c_int64),
+        ("arch", ctypes.c_char * 32),
+    ]
+
+
+# every symbol include/nlh.h declares, with its ctypes signature
+_SIGNATURES = {
+    "nlh_abi_version": ([], ctypes.c_int),
+    "nlh_last_error": ([], ctypes.c_char_p),
+    "nlh_comm_unique_id": ([ctypes.POINTER(ctypes.c_uint8)], ctypes.c_int),
+    "nlh_create": ([ctypes.POINTER(_Params), ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
+    "nlh_destroy": ([ctypes.c_void_p], ctypes.c_int),
+    "nlh_init_test": ([ctypes.c_void_p], ctypes.c_int),
+    "nlh_set_field": ([ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
+    "nlh_get_field": ([ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
+    "nlh_run": ([ctypes.c_void_p, ctypes.c_int64], ctypes.c_int),
+    "nlh_synchronize": ([ctypes.c_void_p], ctypes.c_int),
+    "nlh_step_index": ([ctypes.c_void_p], ctypes.c_int64),
+    "nlh_errors": ([ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_double),
+                    ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
+    "nlh_get_info": ([ctypes.c_void_p, ctypes.POINTER(_Info)], ctypes.c_int),
+    "nlh_kernel_timing": ([ctypes.c_void_p, ctypes.c_int], ctypes.c_int),
+    "nlh_kernel_time": ([ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
+                         ctypes.POINTER(ctypes.c_int64)], ctypes.c_int),
+    "nlh_resolve_owner": ([ctypes.c_int64, ctypes.c_int64, ctypes.c_int32,
+                           ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
+    "nlh_halo_plan": ([ctypes.POINTER(_Params), ctypes.POINTER(ctypes.c_int64), ctypes.c_int64],
+                      ctypes.c_int64),
+}
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load lib/libnlh.so (built by ``make`` / ``__graft_entry__.build()``)."""
+    global _lib
+    if _lib is None:
+        path = lib_path()
+        if not os.path.exists(path):
+            raise NLHError(f"{path} is missing: build it with `make lib` (no CPU fallback exists)")
+        L = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+        for name, (args, res) in _SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = res
+        _lib = L
+    return _lib
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib().nlh_last_error().decode(errors="replace")
+        raise NLHError(f"{what} failed (status {rc}): {msg}")
+
+
+def _dp(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+
+
+def comm_unique_id() -> bytes:
+    buf = (ctypes.c_uint8 * 128)()
+    _check(lib().nlh_comm_unique_id(buf), "nlh_comm_unique_id")
+    return bytes(buf)
+
+
+def resolve_owner(tiles_x: int, tiles_y: int, nranks: int, owner=None) -> np.ndarray:
+    """Tile -> rank map as the library resolves it (reference locidx())."""
+    out = np.empty(tiles_x * tiles_y, dtype=np.int32)
+    oin = None
+    if owner is not None:
+        owner = np.ascontiguousarray(owner, dtype=np.int32)
+        oin = owner.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+    _check(lib().nlh_resolve_owner(tiles_x, tiles_y, nranks, oin,
+                                   out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))), "nlh_resolve_owner")
+    return out
+
+
+def _make_params(nx, ny, eps, k, dt, dh, test, kernel, device, rank, nranks, seg_rows,
+                 tiles, owner, comm_id):
+    p = _Params()
+    p.nx, p.ny, p.eps = int(nx), int(ny), int(eps)
+    p.k, p.dt, p.dh = float(k), float(dt), float(dh)
+    p.test = int(bool(test))
+    p.kernel = _KERNEL_NAMES[kernel] if isinstance(kernel, str) else int(kernel)
+    p.device, p.rank, p.nranks, p.seg_rows = int(device), int(rank), int(nranks), int(seg_rows)
+    p.tiles_x, p.tiles_y = int(tiles[0]), int(tiles[1])
+    keep = []
+    if owner is not None:
+        o = np.ascontiguousarray(owner, dtype=np.int32)
+        keep.append(o)
+        p.owner = o.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+    if comm_id is not None:
+        cid = (ctypes.c_uint8 * 128).from_buffer_copy(comm_id)
+        keep.append(cid)
+        p.comm_id = ctypes.cast(cid, ctypes.POINTER(ctypes.c_uint8))
+    return p, keep
+
+
+def halo_plan(nx, ny, eps, tiles=(1, 1), owner=None, rank=0, nranks=1) -> np.ndarray:
+    """Host-only halo plan: (n, 8) int64 rows
+    {src_rank, dst_rank, gx0, gy0, w, h, src_block, dst_block} received by `rank`."""
+    p, keep = _make_params(nx, ny, eps, 1.0, 1.0, 1.0, 0, KERNEL_AUTO, -1, rank, nranks, 0,
+                           tiles, owner, None)
+    n = lib().nlh_halo_plan(ctypes.byref(p), None, 0)
+    if n < 0:
+        _check(int(-n), "nlh_halo_plan")
+    out = np.zeros((max(n, 0), 8), dtype=np.int64)
+    if n > 0:
+        lib().nlh_halo_plan(ctypes.byref(p), out.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), n)
+    del keep
+    return out
+
+
+def disk_count(eps: int) -> int:
+    """N(eps): lattice points of the closed disk, counted as the reference's
+    loops do (len_1d_line, src/2d_nonlocal_serial.cpp:231,260-262)."""
+    n = 0
+    for dx in range(-eps, eps + 1):
+        n += 2 * int(np.floor(np.sqrt(float(eps * eps - dx * dx)))) + 1
+    return n
+
+
+@dataclass
+class Info:
+    kernel: int
+    device: int
+    nblocks: int
+    npeers: int
+    owned_nodes: int
+    disk_points: int
+    halo_bytes_sent: int
+    device_bytes: int
+    arch: str
+
+
+class Solver:
+    """One rank's share of the 2D nonlocal heat-equation solve on a GPU.
+
+    ``nx, ny`` are GLOBAL lattice sizes.  ``tiles=(tx, ty)`` is the reference's
+    tile grid (np x np for 2d_nonlocal_async, npx x npy for
+    2d_nonlocal_distributed) and ``owner`` its tile -> rank map.
+    """
+
+    def __init__(self, nx, ny, eps, k=1.0, dt=0.0005, dh=0.02, *, test=False, kernel="auto",
+                 device=-1, rank=0, nranks=1, tiles=(1, 1), owner=None, comm_id=None, seg_rows=0):
+        self.nx, self.ny, self.eps = int(nx), int(ny), int(eps)
+        self.k, self.dt, self.dh = float(k), float(dt), float(dh)
+        self.test = bool(test)
+        self.error_l2 = 0.0
+        self.error_linf = 0.0
+        p, keep = _make_params(nx, ny, eps, k, dt, dh, test, kernel, device, rank, nranks,
+                               seg_rows, tiles, owner, comm_id)
+        h = ctypes.c_void_p()
+        _check(lib().nlh_create(ctypes.byref(p), ctypes.byref(h)), "nlh_create")
+        del keep
+        self._h = h
+
+    # -- lifetime --------------------------------------------------------
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            lib().nlh_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # -- reference interface ---------------------------------------------
+    def test_init(self) -> None:
+        self.test = True
+        _check(lib().nlh_init_test(self._h), "nlh_init_test")
+
+    def input_init(self, u: np.ndarray) -> None:
+        """Set u(0) from a global (ny, nx) array (index x + y*nx)."""
+        u = np.ascontiguousarray(u, dtype=np.float64).reshape(self.ny, self.nx)
+        _check(lib().nlh_set_field(self._h, _dp(u)), "nlh_set_field")
+
+    def run(self, nsteps: int) -> None:
+        _check(lib().nlh_run(self._h, int(nsteps)), "nlh_run")
+
+    def synchronize(self) -> None:
+        _check(lib().nlh_synchronize(self._h), "nlh_synchronize")
+
+    def do_work(self, nt: int) -> np.ndarray | None:
+        """Advance nt steps; in test mode also compute error_l2/error_linf at
+        time nt (do_work :293-299).  Returns nothing (use field())."""
+        self.run(nt)
+        self.synchronize()
+        if self.test:
+            t = self.step_index
+            self.error_l2 = self.compute_l2(t)
+            self.error_linf = self.compute_linf(t)
+
+    def _errors(self, time: int):
+        l2 = ctypes.c_double()
+        li = ctypes.c_double()
+        _check(lib().nlh_errors(self._h, int(time), ctypes.byref(l2), ctypes.byref(li)), "nlh_errors")
+        return l2.value, li.value
+
+    def compute_l2(self, time: int) -> float:
+        return self._errors(time)[0]
+
+    def compute_linf(self, time: int) -> float:
+        return self._errors(time)[1]
+
+    def errors(self, time: int):
+        return self._errors(time)
+
+    def field(self, out: np.ndarray | None = None) -> np.ndarray:
+        """Owned nodes of the current field in a global (ny, nx) array."""
+        if out is None:
+            out = np.zeros((self.ny, self.nx), dtype=np.float64)
+        _check(lib().nlh_get_field(self._h, _dp(out)), "nlh_get_field")
+        return out
+
+    @property
+    def step_index(self) -> int:
+        return int(lib().nlh_step_index(self._h))
+
+    def info(self) -> Info:
+        i = _Info()
+        _check(lib().nlh_get_info(self._h, ctypes.byref(i)), "nlh_get_info")
+        return Info(i.kernel, i.device, i.nblocks, i.npeers, i.owned_nodes, i.disk_points,
+                    i.halo_bytes_sent, i.device_bytes, i.arch.decode())
+
+    def kernel_timing(self, enable: bool) -> None:
+        _check(lib().nlh_kernel_timing(self._h, int(bool(enable))), "nlh_kernel_timing")
+
+    def kernel_time(self):
+        ms = ctypes.c_double()
+        n = ctypes.c_int64()
+        _check(lib().nlh_kernel_time(self._h, ctypes.byref(ms), ctypes.byref(n)), "nlh_kernel_time")
+        return ms.value, n.value
+
+
+@dataclass
+class BatchRow:
+    nx: int
+    ny: int
+    nt: int
+    eps: int
+    k: float
+    dt: float
+    dh: float
+    tiles: tuple = (1, 1)
+
+
+def parse_batch(text: str, fmt: str = "serial") -> list[BatchRow]:
+    """Parse a reference batch file (CMakeLists.txt:92-154 formats).
+
+    serial       nx ny nt eps k dt dh            (tests/2d.txt)
+    async        nx ny np nt eps k dt dh         (tests/2d_async.txt; tile dims)
+    distributed  nx ny npx npy nt eps k dt dh    (tests/2d_distributed.txt)
+    Global lattice = tile dims x tile counts for the tiled formats.
+    """
+    tok = text.split()
+    n = int(tok[0])
+    width = {"serial": 7, "async": 8, "distributed": 9}[fmt]
+    rows = []
+    for i in range(n):
+        f = tok[1 + i * width: 1 + (i + 1) * width]
+        if fmt == "serial":
+            nx, ny, nt, eps = map(int, f[:4])
+            k, dt, dh = map(float, f[4:])
+            rows.append(BatchRow(nx, ny, nt, eps, k, dt, dh))
+        elif fmt == "async":
+            nx, ny, npp, nt, eps = map(int, f[:5])
+            k, dt, dh = map(float, f[5:])
+            rows.append(BatchRow(nx * npp, ny * npp, nt, eps, k, dt, dh, (npp, npp)))
+        else:
+            nx, ny, npx, npy, nt, eps = map(int, f[:6])
+            k, dt, dh = map(float, f[6:])
+            rows.append(BatchRow(nx * npx, ny * npy, nt, eps, k, dt, dh, (npx, npy)))
+    return rows
+
+
+def batch_tester(text: str, fmt: str = "serial", kernel="auto") -> str:
+    """Run a reference batch file; "Tests Passed" iff every row has
+    error_l2 / N <= 1e-6 (src/2d_nonlocal_serial.cpp:306-333)."""
+    for r in parse_batch(text, fmt):
+        with Solver(r.nx, r.ny, r.eps, r.k, r.dt, r.dh, test=True, kernel=kernel, tiles=r.tiles) as s:
+            s.test_init()
+            s.do_work(r.nt)
+            if s.error_l2 / float(r.nx * r.ny) > 1e-6:
+                return "Tests Failed"
+    return "Tests Passed"

@@ -1,0 +1,778 @@
+// nlh_api.cpp -- C ABI of libnlh (include/nlh.h): device memory, streams,
+// per-step orchestration, halo exchange over RCCL and error norms.
+//
+// One explicit-Euler step (reference do_work, src/2d_nonlocal_serial.cpp:
+// 273-303; tile form src/2d_nonlocal_distributed.cpp:1146-1262):
+//
+//   single block (1 GPU): one stencil launch over the whole block.  The
+//     out-of-domain halo is a static zero frame, so no exchange happens.
+//
+//   several blocks / ranks:
+//     comm stream : pack halo pieces for other ranks -> grouped ncclSend /
+//                   ncclRecv per peer -> unpack + local block-to-block copies
+//     main stream : interior kernel (nodes whose disk lies inside the block,
+//                   the reference's "interior" of :1156-1178) overlapped with
+//                   the exchange, then the boundary bands (:1180-1259) once
+//                   the halo event fires.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "nlh.h"
+#include "nlh_device.h"
+#include "nlh_plan.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                        \
+  do {                                                                       \
+    hipError_t e_ = (expr);                                                  \
+    if (e_ != hipSuccess)                                                    \
+      return fail(NLH_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+#define NCCL_TRY(expr)                                                       \
+  do {                                                                       \
+    ncclResult_t r_ = (expr);                                                \
+    if (r_ != ncclSuccess)                                                   \
+      return fail(NLH_ERR_RCCL, std::string(#expr) + ": " + ncclGetErrorString(r_)); \
+  } while (0)
+
+int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
+int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+struct LocalBlock {
+  int plan_index = 0;
+  nlh::GRect r;
+  int64_t pitch = 0, rows = 0;
+  int32_t xl = 0;
+  double *base[2] = {nullptr, nullptr};
+  double *lw_base = nullptr;
+  double *origin(int k) const { return base[k] + (int64_t)(rows - r.h) / 2 * pitch + xl; }
+  double *lw_origin() const { return lw_base ? lw_base + (int64_t)(rows - r.h) / 2 * pitch + xl : nullptr; }
+  // band flags: halo on that side depends on other blocks
+  bool L = false, Rr = false, T = false, B = false;
+};
+
+struct Peer {
+  int rank = 0;
+  int64_t send_count = 0, recv_count = 0;  // doubles
+  double *send = nullptr, *recv = nullptr;
+};
+
+}  // namespace
+
+struct nlh_solver {
+  nlh_params p{};
+  std::vector<int32_t> owner;
+  nlh::Plan plan;
+  std::vector<LocalBlock> blocks;
+  int device = 0;
+  int kernel = NLH_KERNEL_EXACT;
+  hipStream_t s_main = nullptr, s_comm = nullptr;
+  hipEvent_t ev_ready = nullptr, ev_halo = nullptr;
+  int64_t t = 0;
+  int cur = 0;
+  double *d_sxt = nullptr, *d_syt = nullptr;
+  int32_t *d_lens = nullptr;
+  nlh::StepConst sc{};
+  int64_t disk = 0;
+  bool exchange = false;
+  nlh::RectList rl_full[2]{}, rl_int[2]{}, rl_bnd[2]{};
+  // halo exchange
+  ncclComm_t comm = nullptr;
+  std::vector<Peer> peers;
+  nlh::CopyList cl_pack[2]{}, cl_unpack[2]{}, cl_local[2]{};
+  int64_t halo_bytes = 0;
+  // norms
+  nlh::NormPartial *d_part = nullptr;
+  std::vector<int> part_off;
+  int part_total = 0;
+  double *d_red = nullptr;
+  // timing
+  bool timing = false;
+  std::vector<hipEvent_t> ev_pool;
+  size_t ev_used = 0;
+  int64_t device_bytes = 0;
+  char arch[32] = {0};
+};
+
+namespace {
+
+int set_device(const nlh_solver *s) {
+  HIP_TRY(hipSetDevice(s->device));
+  return NLH_OK;
+}
+
+void fill_rect_common(nlh::Rect &R, const LocalBlock &b, int k, const nlh_solver *s) {
+  R.u = b.origin(k);
+  R.un = b.origin(1 - k);
+  R.lw = b.lw_origin();
+  R.pitch = b.pitch;
+  R.gx0 = (int32_t)b.r.x0;
+  R.gy0 = (int32_t)b.r.y0;
+  (void)s;
+}
+
+// split one block into interior + bands (interior first)
+struct LRect { int x0, y0, x1, y1; bool interior; };
+
+std::vector<LRect> split_block(const LocalBlock &b, int E, int sw) {
+  const int bx = (int)b.r.w, by = (int)b.r.h;
+  std::vector<LRect> out;
+  if (!(b.L || b.Rr || b.T || b.B)) {
+    out.push_back({0, 0, bx, by, true});
+    return out;
+  }
+  int a = b.L ? std::min(sw, bx) : 0;
+  if (b.L && a < E) a = std::min(E, bx);
+  int bb = bx;
+  if (b.Rr) {
+    const int lim = bx - E;
+    bb = lim <= a ? a : a + (lim - a) / sw * sw;
+  }
+  int yt = b.T ? std::min(E, by) : 0;
+  int yb = b.B ? std::max(by - E, yt) : by;
+  if (bb > a && yb > yt) out.push_back({a, yt, bb, yb, true});
+  if (a > 0) out.push_back({0, 0, a, by, false});
+  if (bb < bx) out.push_back({bb, 0, bx, by, false});
+  if (bb > a && yt > 0) out.push_back({a, 0, bb, yt, false});
+  if (bb > a && yb < by) out.push_back({a, yb, bb, by, false});
+  return out;
+}
+
+int build_rectlists(nlh_solver *s) {
+  const int E = (int)s->p.eps;
+  const bool fast = s->kernel == NLH_KERNEL_FAST;
+  const int sw = fast ? nlh::fast_strip_width(E) : 64;
+  // gather local rects
+  struct Item { int blk; LRect r; };
+  std::vector<Item> all, inter, bnd;
+  for (size_t bi = 0; bi < s->blocks.size(); ++bi) {
+    for (auto &r : split_block(s->blocks[bi], E, sw)) {
+      Item it{(int)bi, r};
+      all.push_back(it);
+      (r.interior ? inter : bnd).push_back(it);
+    }
+  }
+  // segment height for the fast kernel: aim at ~2048 single-wave workgroups
+  int seg_h = 4;
+  if (fast) {
+    int64_t strip_rows = 0;
+    for (auto &it : all) strip_rows += ceil_div(it.r.x1 - it.r.x0, sw) * (it.r.y1 - it.r.y0);
+    seg_h = s->p.seg_rows > 0 ? s->p.seg_rows
+                              : (int)std::max<int64_t>(nlh::fast_seg_min(E), ceil_div(strip_rows, 2048));
+  }
+  s->sc.seg_h = seg_h;
+  auto make = [&](const std::vector<Item> &items, int k, nlh::RectList &rl) -> int {
+    std::memset(&rl, 0, sizeof(rl));
+    // when not exchanging, one launch covers every rect of every block
+    int w = 0;
+    for (auto &it : items) {
+      if (rl.nrects >= nlh::kMaxRects)
+        return fail(NLH_ERR_UNSUPPORTED, "too many output rectangles on this rank");
+      nlh::Rect &R = rl.r[rl.nrects++];
+      fill_rect_common(R, s->blocks[it.blk], k, s);
+      R.x0 = it.r.x0; R.y0 = it.r.y0; R.x1 = it.r.x1; R.y1 = it.r.y1;
+      if (fast) {
+        R.nstrip = (int)ceil_div(R.x1 - R.x0, sw);
+        R.nseg = (int)ceil_div(R.y1 - R.y0, seg_h);
+      } else {
+        R.nstrip = (int)ceil_div(R.x1 - R.x0, 64);
+        R.nseg = (int)ceil_div(R.y1 - R.y0, 4);
+      }
+      R.wg_begin = w;
+      w += R.nstrip * R.nseg;
+    }
+    rl.nwork = w;
+    return NLH_OK;
+  };
+  for (int k = 0; k < 2; ++k) {
+    int rc;
+    if ((rc = make(all, k, s->rl_full[k])) != NLH_OK) return rc;
+    if ((rc = make(inter, k, s->rl_int[k])) != NLH_OK) return rc;
+    if ((rc = make(bnd, k, s->rl_bnd[k])) != NLH_OK) return rc;
+  }
+  return NLH_OK;
+}
+
+int add_copy(nlh::CopyList &cl, const double *src, int64_t spitch, double *dst,
+             int64_t dpitch, int64_t w, int64_t h) {
+  if (w <= 0 || h <= 0) return NLH_OK;
+  if (cl.ncopies >= nlh::kMaxCopies)
+    return fail(NLH_ERR_UNSUPPORTED, "too many halo pieces on this rank");
+  nlh::Copy &c = cl.c[cl.ncopies++];
+  c.src = src;
+  c.dst = dst;
+  c.spitch = spitch;
+  c.dpitch = dpitch;
+  c.w = (int32_t)w;
+  c.h = (int32_t)h;
+  c.wg_begin = cl.nwork;
+  cl.nwork += (int32_t)ceil_div(w * h, 256);
+  return NLH_OK;
+}
+
+// pointer to global node (gx, gy) inside local block b, parity k
+double *node_ptr(const LocalBlock &b, int k, int64_t gx, int64_t gy) {
+  return b.origin(k) + (gy - b.r.y0) * b.pitch + (gx - b.r.x0);
+}
+
+int build_exchange(nlh_solver *s) {
+  const int me = s->p.rank;
+  std::map<int, size_t> local_of_plan;  // plan block index -> local index
+  for (size_t i = 0; i < s->blocks.size(); ++i) local_of_plan[s->blocks[i].plan_index] = i;
+  // peers and message sizes in plan order
+  std::map<int, Peer> peers;
+  for (auto &pc : s->plan.pieces) {
+    if (pc.src_rank == me && pc.dst_rank != me) peers[pc.dst_rank].send_count += pc.r.w * pc.r.h;
+    if (pc.dst_rank == me && pc.src_rank != me) peers[pc.src_rank].recv_count += pc.r.w * pc.r.h;
+  }
+  for (auto &kv : peers) {
+    Peer &pr = kv.second;
+    pr.rank = kv.first;
+    if (pr.send_count) HIP_TRY(hipMalloc(&pr.send, pr.send_count * sizeof(double)));
+    if (pr.recv_count) HIP_TRY(hipMalloc(&pr.recv, pr.recv_count * sizeof(double)));
+    s->device_bytes += (pr.send_count + pr.recv_count) * (int64_t)sizeof(double);
+    s->halo_bytes += pr.send_count * (int64_t)sizeof(double);
+  }
+  for (int k = 0; k < 2; ++k) {
+    std::map<int, int64_t> soff, roff;
+    nlh::CopyList &pk = s->cl_pack[k], &up = s->cl_unpack[k], &lc = s->cl_local[k];
+    std::memset(&pk, 0, sizeof(pk));
+    std::memset(&up, 0, sizeof(up));
+    std::memset(&lc, 0, sizeof(lc));
+    for (auto &pc : s->plan.pieces) {
+      const int64_t n = pc.r.w * pc.r.h;
+      int rc = NLH_OK;
+      if (pc.src_rank == me && pc.dst_rank == me) {
+        const LocalBlock &sb = s->blocks[local_of_plan[pc.src_block]];
+        const LocalBlock &db = s->blocks[local_of_plan[pc.dst_block]];
+        rc = add_copy(lc, node_ptr(sb, k, pc.r.x0, pc.r.y0), sb.pitch,
+                      node_ptr(db, k, pc.r.x0, pc.r.y0), db.pitch, pc.r.w, pc.r.h);
+      } else if (pc.src_rank == me) {
+        const LocalBlock &sb = s->blocks[local_of_plan[pc.src_block]];
+        Peer &pr = peers[pc.dst_rank];
+        rc = add_copy(pk, node_ptr(sb, k, pc.r.x0, pc.r.y0), sb.pitch,
+                      pr.send + soff[pc.dst_rank], pc.r.w, pc.r.w, pc.r.h);
+        soff[pc.dst_rank] += n;
+      } else if (pc.dst_rank == me) {
+        const LocalBlock &db = s->blocks[local_of_plan[pc.dst_block]];
+        Peer &pr = peers[pc.src_rank];
+        rc = add_copy(up, pr.recv + roff[pc.src_rank], pc.r.w,
+                      node_ptr(db, k, pc.r.x0, pc.r.y0), db.pitch, pc.r.w, pc.r.h);
+        roff[pc.src_rank] += n;
+      }
+      if (rc != NLH_OK) return rc;
+    }
+  }
+  for (auto &kv : peers) s->peers.push_back(kv.second);
+  s->exchange = !s->plan.pieces.empty();
+  return NLH_OK;
+}
+
+hipEvent_t pool_event(nlh_solver *s) {
+  if (s->ev_used == s->ev_pool.size()) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    s->ev_pool.push_back(e);
+  }
+  return s->ev_pool[s->ev_used++];
+}
+
+int launch_stencil(nlh_solver *s, const nlh::RectList &rl) {
+  if (rl.nwork == 0) return NLH_OK;
+  int rc;
+  const bool test = s->p.test != 0;
+  if (s->kernel == NLH_KERNEL_FAST)
+    rc = nlh::launch_fast(rl, s->sc, test, s->s_main);
+  else
+    rc = nlh::launch_exact(rl, s->sc, test, s->s_main);
+  if (rc != 0) return fail(NLH_ERR_HIP, std::string("stencil launch failed: ") + hipGetErrorString((hipError_t)rc));
+  return NLH_OK;
+}
+
+void set_time(nlh_solver *s, int64_t t) {
+  // (2*M_PI)*(time*dt) exactly as the reference spells it (:208, :237)
+  const double arg = 2 * M_PI * (t * s->p.dt);
+  s->sc.st2pi = 2 * M_PI * sin(arg);
+  s->sc.ct = cos(arg);
+}
+
+int enqueue_step(nlh_solver *s) {
+  const int k = s->cur;
+  set_time(s, s->t);
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (s->timing) {
+    e0 = pool_event(s);
+    e1 = pool_event(s);
+    if (!e0 || !e1) return fail(NLH_ERR_HIP, "event pool");
+  }
+  if (!s->exchange) {
+    if (e0) HIP_TRY(hipEventRecord(e0, s->s_main));
+    int rc = launch_stencil(s, s->rl_full[k]);
+    if (rc) return rc;
+    if (e1) HIP_TRY(hipEventRecord(e1, s->s_main));
+  } else {
+    HIP_TRY(hipEventRecord(s->ev_ready, s->s_main));
+    HIP_TRY(hipStreamWaitEvent(s->s_comm, s->ev_ready, 0));
+    if (nlh::launch_copies(s->cl_pack[k], s->s_comm)) return fail(NLH_ERR_HIP, "pack launch");
+    if (!s->peers.empty()) {
+      NCCL_TRY(ncclGroupStart());
+      for (auto &pr : s->peers) {
+        if (pr.send_count) NCCL_TRY(ncclSend(pr.send, pr.send_count, ncclDouble, pr.rank, s->comm, s->s_comm));
+        if (pr.recv_count) NCCL_TRY(ncclRecv(pr.recv, pr.recv_count, ncclDouble, pr.rank, s->comm, s->s_comm));
+      }
+      NCCL_TRY(ncclGroupEnd());
+    }
+    if (nlh::launch_copies(s->cl_unpack[k], s->s_comm)) return fail(NLH_ERR_HIP, "unpack launch");
+    if (nlh::launch_copies(s->cl_local[k], s->s_comm)) return fail(NLH_ERR_HIP, "local halo launch");
+    HIP_TRY(hipEventRecord(s->ev_halo, s->s_comm));
+    if (e0) HIP_TRY(hipEventRecord(e0, s->s_main));
+    int rc = launch_stencil(s, s->rl_int[k]);
+    if (rc) return rc;
+    HIP_TRY(hipStreamWaitEvent(s->s_main, s->ev_halo, 0));
+    rc = launch_stencil(s, s->rl_bnd[k]);
+    if (rc) return rc;
+    if (e1) HIP_TRY(hipEventRecord(e1, s->s_main));
+  }
+  s->cur = 1 - k;
+  s->t += 1;
+  return NLH_OK;
+}
+
+int compute_lw(nlh_solver *s) {
+  // L_h[W0](x) = sum_disk c*(W0~_j - W0_x)*dh^2 with the exact per-term
+  // order; the fast test-mode source is then b = -(2pi st) W0 - ct L_h[W0]
+  for (auto &b : s->blocks) {
+    double *tmp = b.base[1];
+    if (nlh::launch_fill_w0(tmp, b.pitch, b.xl, (int)b.r.w, (int)b.r.h, (int)b.r.x0,
+                            (int)b.r.y0, s->sc, s->s_main))
+      return fail(NLH_ERR_HIP, "fill_w0 launch");
+    nlh::RectList rl{};
+    rl.nrects = 1;
+    nlh::Rect &R = rl.r[0];
+    R.u = b.origin(1);
+    R.un = b.lw_origin();
+    R.pitch = b.pitch;
+    R.gx0 = (int32_t)b.r.x0;
+    R.gy0 = (int32_t)b.r.y0;
+    R.x0 = 0; R.y0 = 0; R.x1 = (int)b.r.w; R.y1 = (int)b.r.h;
+    R.nstrip = (int)ceil_div(b.r.w, 64);
+    R.nseg = (int)ceil_div(b.r.h, 4);
+    rl.nwork = R.nstrip * R.nseg;
+    if (nlh::launch_exact_sum(rl, s->sc, s->s_main)) return fail(NLH_ERR_HIP, "L_h[W0] launch");
+    HIP_TRY(hipMemsetAsync(b.base[1], 0, b.pitch * b.rows * sizeof(double), s->s_main));
+  }
+  HIP_TRY(hipStreamSynchronize(s->s_main));
+  return NLH_OK;
+}
+
+int destroy_impl(nlh_solver *s) {
+  if (!s) return NLH_OK;
+  hipSetDevice(s->device);
+  if (s->s_main) hipStreamSynchronize(s->s_main);
+  if (s->s_comm) hipStreamSynchronize(s->s_comm);
+  if (s->comm) ncclCommDestroy(s->comm);
+  for (auto &b : s->blocks) {
+    hipFree(b.base[0]);
+    hipFree(b.base[1]);
+    hipFree(b.lw_base);
+  }
+  for (auto &pr : s->peers) {
+    hipFree(pr.send);
+    hipFree(pr.recv);
+  }
+  hipFree(s->d_sxt);
+  hipFree(s->d_syt);
+  hipFree(s->d_lens);
+  hipFree(s->d_part);
+  hipFree(s->d_red);
+  for (auto e : s->ev_pool) hipEventDestroy(e);
+  if (s->ev_ready) hipEventDestroy(s->ev_ready);
+  if (s->ev_halo) hipEventDestroy(s->ev_halo);
+  if (s->s_main) hipStreamDestroy(s->s_main);
+  if (s->s_comm) hipStreamDestroy(s->s_comm);
+  delete s;
+  return NLH_OK;
+}
+
+int create_impl(const nlh_params *pin, nlh_solver *s) {
+  const nlh_params &p = *pin;
+  if (p.nx <= 0 || p.ny <= 0) return fail(NLH_ERR_ARG, "nx, ny must be positive");
+  if (p.eps < 1) return fail(NLH_ERR_ARG, "eps must be >= 1");
+  if (p.nx + 2 * p.eps > (1ll << 30) || p.ny + 2 * p.eps > (1ll << 30))
+    return fail(NLH_ERR_ARG, "lattice too large for 32-bit node coordinates");
+  if (p.nranks < 1 || p.rank < 0 || p.rank >= p.nranks) return fail(NLH_ERR_ARG, "bad rank/nranks");
+  const int64_t tx = p.tiles_x > 0 ? p.tiles_x : 1, ty = p.tiles_y > 0 ? p.tiles_y : 1;
+  if (p.nx % tx || p.ny % ty) return fail(NLH_ERR_ARG, "tiles_x/tiles_y must divide nx/ny");
+  if (p.kernel < NLH_KERNEL_AUTO || p.kernel > NLH_KERNEL_FAST) return fail(NLH_ERR_ARG, "bad kernel");
+  s->p = p;
+  s->p.tiles_x = tx;
+  s->p.tiles_y = ty;
+  s->p.owner = nullptr;
+  s->p.comm_id = nullptr;
+
+  std::string err;
+  if (!nlh::resolve_owner(tx, ty, p.nranks, p.owner, s->owner, err)) return fail(NLH_ERR_ARG, err);
+  s->plan = nlh::make_plan(p.nx, p.ny, p.eps, tx, ty, s->owner);
+
+  // ---- device
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+    return fail(NLH_ERR_HIP, "no HIP device visible (libnlh has no CPU fallback)");
+  if (p.device >= 0) {
+    if (p.device >= ndev) return fail(NLH_ERR_ARG, "device ordinal out of range");
+    s->device = p.device;
+  } else {
+    HIP_TRY(hipGetDevice(&s->device));
+  }
+  HIP_TRY(hipSetDevice(s->device));
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, s->device));
+  std::snprintf(s->arch, sizeof(s->arch), "%s", prop.gcnArchName);
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(NLH_ERR_UNSUPPORTED, std::string("libnlh is built for gfx950, device is ") + prop.gcnArchName);
+
+  // ---- kernel choice
+  const int E = (int)p.eps;
+  int kern = p.kernel;
+  if (kern == NLH_KERNEL_AUTO) kern = p.test ? NLH_KERNEL_EXACT : NLH_KERNEL_FAST;
+  if (kern == NLH_KERNEL_FAST && !nlh::fast_supported(E)) {
+    if (p.kernel == NLH_KERNEL_FAST)
+      return fail(NLH_ERR_UNSUPPORTED, "fast kernel not instantiated for eps=" + std::to_string(E));
+    kern = NLH_KERNEL_EXACT;
+  }
+  s->kernel = kern;
+
+  HIP_TRY(hipStreamCreateWithFlags(&s->s_main, hipStreamNonBlocking));
+  HIP_TRY(hipStreamCreateWithFlags(&s->s_comm, hipStreamNonBlocking));
+  HIP_TRY(hipEventCreateWithFlags(&s->ev_ready, hipEventDisableTiming));
+  HIP_TRY(hipEventCreateWithFlags(&s->ev_halo, hipEventDisableTiming));
+
+  // ---- constants and host-computed tables (glibc sin, bit-equal to w())
+  std::vector<double> sxt(p.nx + 2 * E), syt(p.ny + 2 * E);
+  for (int64_t g = -E; g < p.nx + E; ++g) sxt[g + E] = sin(2 * M_PI * (g * p.dh));
+  for (int64_t g = -E; g < p.ny + E; ++g) syt[g + E] = sin(2 * M_PI * (g * p.dh));
+  std::vector<int32_t> lens(E + 1);
+  s->disk = 0;
+  for (int d = 0; d <= E; ++d) lens[d] = (int32_t)(long)sqrt((double)((long)E * E - (long)d * d));
+  for (int d = -E; d <= E; ++d) s->disk += 2 * lens[d < 0 ? -d : d] + 1;
+  HIP_TRY(hipMalloc(&s->d_sxt, sxt.size() * sizeof(double)));
+  HIP_TRY(hipMalloc(&s->d_syt, syt.size() * sizeof(double)));
+  HIP_TRY(hipMalloc(&s->d_lens, lens.size() * sizeof(int32_t)));
+  HIP_TRY(hipMemcpy(s->d_sxt, sxt.data(), sxt.size() * sizeof(double), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(s->d_syt, syt.data(), syt.size() * sizeof(double), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(s->d_lens, lens.data(), lens.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+  s->sc.c2d = (p.k * 8) / pow(p.eps * p.dh, 4);
+  s->sc.dh2 = p.dh * p.dh;
+  s->sc.dt = p.dt;
+  s->sc.alpha = s->sc.c2d * s->sc.dh2 * p.dt;
+  s->sc.nf = (double)s->disk;
+  s->sc.sxt = s->d_sxt;
+  s->sc.syt = s->d_syt;
+  s->sc.lens = s->d_lens;
+  s->sc.nx = p.nx;
+  s->sc.ny = p.ny;
+  s->sc.E = E;
+  set_time(s, 0);
+
+  // ---- local blocks, padded (see nlh_device.h)
+  const int64_t XL = round_up(E, 8);
+  for (size_t i = 0; i < s->plan.blocks.size(); ++i) {
+    const auto &bd = s->plan.blocks[i];
+    if (bd.rank != p.rank) continue;
+    LocalBlock b;
+    b.plan_index = (int)i;
+    b.r = bd.r;
+    b.xl = (int32_t)XL;
+    b.pitch = XL + round_up(b.r.w, 128) + XL;
+    b.rows = b.r.h + 2 * E;
+    b.L = b.r.x0 > 0;
+    b.Rr = b.r.x0 + b.r.w < p.nx;
+    b.T = b.r.y0 > 0;
+    b.B = b.r.y0 + b.r.h < p.ny;
+    const size_t bytes = (size_t)(b.pitch * b.rows) * sizeof(double);
+    for (int k = 0; k < 2; ++k) {
+      HIP_TRY(hipMalloc(&b.base[k], bytes));
+      HIP_TRY(hipMemset(b.base[k], 0, bytes));
+      s->device_bytes += (int64_t)bytes;
+    }
+    if (kern == NLH_KERNEL_FAST && p.test) {
+      HIP_TRY(hipMalloc(&b.lw_base, bytes));
+      HIP_TRY(hipMemset(b.lw_base, 0, bytes));
+      s->device_bytes += (int64_t)bytes;
+    }
+    s->blocks.push_back(b);
+  }
+  if (s->blocks.size() > (size_t)nlh::kMaxRects)
+    return fail(NLH_ERR_UNSUPPORTED, "too many blocks on one rank");
+
+  int rc = build_rectlists(s);
+  if (rc) return rc;
+
+  // ---- RCCL communicator and exchange plan
+  if (p.nranks > 1) {
+    if (!p.comm_id) return fail(NLH_ERR_ARG, "nranks > 1 requires comm_id");
+    ncclUniqueId id;
+    static_assert(sizeof(ncclUniqueId) == NLH_COMM_ID_BYTES, "unique id size");
+    std::memcpy(&id, p.comm_id, sizeof(id));
+    NCCL_TRY(ncclCommInitRank(&s->comm, p.nranks, id, p.rank));
+  }
+  rc = build_exchange(s);
+  if (rc) return rc;
+  if (s->exchange && p.nranks == 1 && !s->peers.empty())
+    return fail(NLH_ERR_STATE, "internal: peers without communicator");
+
+  // ---- norm scratch
+  int tot = 0;
+  for (auto &b : s->blocks) {
+    s->part_off.push_back(tot);
+    tot += nlh::norm_workgroups((int)b.r.w, (int)b.r.h);
+  }
+  s->part_total = tot;
+  HIP_TRY(hipMalloc(&s->d_part, std::max(tot, 1) * sizeof(nlh::NormPartial)));
+  HIP_TRY(hipMalloc(&s->d_red, 2 * sizeof(double)));
+
+  if (kern == NLH_KERNEL_FAST && p.test) {
+    rc = compute_lw(s);
+    if (rc) return rc;
+  }
+  return NLH_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int nlh_abi_version(void) { return NLH_ABI_VERSION; }
+
+const char *nlh_last_error(void) { return g_err.c_str(); }
+
+int nlh_comm_unique_id(uint8_t id[NLH_COMM_ID_BYTES]) {
+  if (!id) return fail(NLH_ERR_ARG, "null id");
+  ncclUniqueId u;
+  NCCL_TRY(ncclGetUniqueId(&u));
+  std::memcpy(id, &u, sizeof(u));
+  return NLH_OK;
+}
+
+int nlh_create(const nlh_params *p, nlh_solver **out) {
+  if (!p || !out) return fail(NLH_ERR_ARG, "null argument");
+  *out = nullptr;
+  nlh_solver *s = new nlh_solver();
+  int rc = create_impl(p, s);
+  if (rc != NLH_OK) {
+    const std::string keep = g_err;
+    destroy_impl(s);
+    g_err = keep;
+    return rc;
+  }
+  *out = s;
+  return NLH_OK;
+}
+
+int nlh_destroy(nlh_solver *s) { return destroy_impl(s); }
+
+int nlh_init_test(nlh_solver *s) {
+  if (!s) return fail(NLH_ERR_ARG, "null solver");
+  int rc = set_device(s);
+  if (rc) return rc;
+  HIP_TRY(hipStreamSynchronize(s->s_comm));
+  s->cur = 0;
+  s->t = 0;
+  for (auto &b : s->blocks)
+    if (nlh::launch_init_test(b.origin(0), b.pitch, (int)b.r.w, (int)b.r.h, (int)b.r.x0,
+                              (int)b.r.y0, s->sc, s->s_main))
+      return fail(NLH_ERR_HIP, "init launch");
+  HIP_TRY(hipStreamSynchronize(s->s_main));
+  return NLH_OK;
+}
+
+int nlh_set_field(nlh_solver *s, const double *u) {
+  if (!s || !u) return fail(NLH_ERR_ARG, "null argument");
+  int rc = set_device(s);
+  if (rc) return rc;
+  HIP_TRY(hipStreamSynchronize(s->s_comm));
+  HIP_TRY(hipStreamSynchronize(s->s_main));
+  s->cur = 0;
+  s->t = 0;
+  for (auto &b : s->blocks)
+    HIP_TRY(hipMemcpy2D(b.origin(0), b.pitch * sizeof(double), u + b.r.y0 * s->p.nx + b.r.x0,
+                        s->p.nx * sizeof(double), b.r.w * sizeof(double), b.r.h,
+                        hipMemcpyHostToDevice));
+  return NLH_OK;
+}
+
+int nlh_get_field(nlh_solver *s, double *u) {
+  if (!s || !u) return fail(NLH_ERR_ARG, "null argument");
+  int rc = set_device(s);
+  if (rc) return rc;
+  HIP_TRY(hipStreamSynchronize(s->s_comm));
+  HIP_TRY(hipStreamSynchronize(s->s_main));
+  for (auto &b : s->blocks)
+    HIP_TRY(hipMemcpy2D(u + b.r.y0 * s->p.nx + b.r.x0, s->p.nx * sizeof(double), b.origin(s->cur),
+                        b.pitch * sizeof(double), b.r.w * sizeof(double), b.r.h,
+                        hipMemcpyDeviceToHost));
+  return NLH_OK;
+}
+
+int nlh_run(nlh_solver *s, int64_t nsteps) {
+  if (!s) return fail(NLH_ERR_ARG, "null solver");
+  if (nsteps < 0) return fail(NLH_ERR_ARG, "negative step count");
+  int rc = set_device(s);
+  if (rc) return rc;
+  for (int64_t i = 0; i < nsteps; ++i) {
+    rc = enqueue_step(s);
+    if (rc) return rc;
+  }
+  return NLH_OK;
+}
+
+int nlh_synchronize(nlh_solver *s) {
+  if (!s) return fail(NLH_ERR_ARG, "null solver");
+  int rc = set_device(s);
+  if (rc) return rc;
+  HIP_TRY(hipStreamSynchronize(s->s_comm));
+  HIP_TRY(hipStreamSynchronize(s->s_main));
+  return NLH_OK;
+}
+
+int64_t nlh_step_index(const nlh_solver *s) { return s ? s->t : -1; }
+
+int nlh_errors(nlh_solver *s, int64_t time, double *l2, double *linf) {
+  if (!s || !l2 || !linf) return fail(NLH_ERR_ARG, "null argument");
+  int rc = set_device(s);
+  if (rc) return rc;
+  HIP_TRY(hipStreamSynchronize(s->s_comm));
+  const double save_st = s->sc.st2pi, save_ct = s->sc.ct;
+  set_time(s, time);
+  for (size_t i = 0; i < s->blocks.size(); ++i) {
+    const auto &b = s->blocks[i];
+    if (nlh::launch_norms(b.origin(s->cur), b.pitch, (int)b.r.w, (int)b.r.h, (int)b.r.x0,
+                          (int)b.r.y0, s->sc, s->d_part + s->part_off[i], s->s_main))
+      return fail(NLH_ERR_HIP, "norm launch");
+  }
+  s->sc.st2pi = save_st;
+  s->sc.ct = save_ct;
+  std::vector<nlh::NormPartial> h(std::max(s->part_total, 1));
+  if (s->part_total)
+    HIP_TRY(hipMemcpyAsync(h.data(), s->d_part, s->part_total * sizeof(nlh::NormPartial),
+                           hipMemcpyDeviceToHost, s->s_main));
+  HIP_TRY(hipStreamSynchronize(s->s_main));
+  double e2 = 0.0, ei = 0.0;
+  for (int i = 0; i < s->part_total; ++i) {
+    e2 += h[i].l2;
+    ei = std::max(ei, h[i].linf);
+  }
+  if (s->comm) {
+    double v[2] = {e2, ei};
+    HIP_TRY(hipMemcpyAsync(s->d_red, v, 2 * sizeof(double), hipMemcpyHostToDevice, s->s_comm));
+    NCCL_TRY(ncclGroupStart());
+    NCCL_TRY(ncclAllReduce(s->d_red, s->d_red, 1, ncclDouble, ncclSum, s->comm, s->s_comm));
+    NCCL_TRY(ncclAllReduce(s->d_red + 1, s->d_red + 1, 1, ncclDouble, ncclMax, s->comm, s->s_comm));
+    NCCL_TRY(ncclGroupEnd());
+    HIP_TRY(hipMemcpyAsync(v, s->d_red, 2 * sizeof(double), hipMemcpyDeviceToHost, s->s_comm));
+    HIP_TRY(hipStreamSynchronize(s->s_comm));
+    e2 = v[0];
+    ei = v[1];
+  }
+  *l2 = e2;
+  *linf = ei;
+  return NLH_OK;
+}
+
+int nlh_get_info(const nlh_solver *s, nlh_info *info) {
+  if (!s || !info) return fail(NLH_ERR_ARG, "null argument");
+  std::memset(info, 0, sizeof(*info));
+  info->kernel = s->kernel;
+  info->device = s->device;
+  info->nblocks = (int32_t)s->blocks.size();
+  info->npeers = (int32_t)s->peers.size();
+  for (auto &b : s->blocks) info->owned_nodes += b.r.w * b.r.h;
+  info->disk_points = s->disk;
+  info->halo_bytes_sent = s->halo_bytes;
+  info->device_bytes = s->device_bytes;
+  std::snprintf(info->arch, sizeof(info->arch), "%s", s->arch);
+  return NLH_OK;
+}
+
+int nlh_kernel_timing(nlh_solver *s, int enable) {
+  if (!s) return fail(NLH_ERR_ARG, "null solver");
+  int rc = set_device(s);
+  if (rc) return rc;
+  HIP_TRY(hipStreamSynchronize(s->s_main));
+  s->timing = enable != 0;
+  s->ev_used = 0;
+  return NLH_OK;
+}
+
+int nlh_kernel_time(nlh_solver *s, double *total_ms, int64_t *launches) {
+  if (!s || !total_ms || !launches) return fail(NLH_ERR_ARG, "null argument");
+  int rc = set_device(s);
+  if (rc) return rc;
+  HIP_TRY(hipStreamSynchronize(s->s_main));
+  double tot = 0.0;
+  for (size_t i = 0; i + 1 < s->ev_used; i += 2) {
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, s->ev_pool[i], s->ev_pool[i + 1]));
+    tot += ms;
+  }
+  *total_ms = tot;
+  *launches = (int64_t)(s->ev_used / 2);
+  return NLH_OK;
+}
+
+int nlh_resolve_owner(int64_t tiles_x, int64_t tiles_y, int32_t nranks,
+                      const int32_t *owner_in, int32_t *owner_out) {
+  if (tiles_x < 1 || tiles_y < 1 || nranks < 1 || !owner_out) return fail(NLH_ERR_ARG, "bad argument");
+  std::vector<int32_t> o;
+  std::string err;
+  if (!nlh::resolve_owner(tiles_x, tiles_y, nranks, owner_in, o, err)) return fail(NLH_ERR_ARG, err);
+  std::memcpy(owner_out, o.data(), o.size() * sizeof(int32_t));
+  return NLH_OK;
+}
+
+int64_t nlh_halo_plan(const nlh_params *p, int64_t *pieces, int64_t cap) {
+  if (!p) return -fail(NLH_ERR_ARG, "null params");
+  const int64_t tx = p->tiles_x > 0 ? p->tiles_x : 1, ty = p->tiles_y > 0 ? p->tiles_y : 1;
+  if (p->nx <= 0 || p->ny <= 0 || p->nx % tx || p->ny % ty || p->nranks < 1)
+    return -fail(NLH_ERR_ARG, "bad lattice / tile grid");
+  std::vector<int32_t> o;
+  std::string err;
+  if (!nlh::resolve_owner(tx, ty, p->nranks, p->owner, o, err)) return -fail(NLH_ERR_ARG, err);
+  nlh::Plan plan = nlh::make_plan(p->nx, p->ny, p->eps, tx, ty, o);
+  int64_t n = 0;
+  for (auto &pc : plan.pieces) {
+    if (pc.dst_rank != p->rank) continue;
+    if (pieces && n < cap) {
+      int64_t *r = pieces + 8 * n;
+      r[0] = pc.src_rank;
+      r[1] = pc.dst_rank;
+      r[2] = pc.r.x0;
+      r[3] = pc.r.y0;
+      r[4] = pc.r.w;
+      r[5] = pc.r.h;
+      r[6] = pc.src_block;
+      r[7] = pc.dst_block;
+    }
+    ++n;
+  }
+  return n;
+}
+
+}  // extern "C"

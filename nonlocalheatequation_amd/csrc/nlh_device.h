@@ -1,0 +1,103 @@
+// nlh_device.h -- structures shared by the host orchestration (nlh_api.cpp)
+// and the gfx950 kernels (nlh_kernels.hip), plus the internal launch API.
+//
+// HBM layout of one block (a rectangle of owned nodes, bx x by):
+//   padded rows  y in [-E, by+E)        E = eps
+//   padded cols  x in [-XL, pitch-XL)   XL = round_up(eps, 8)
+//   node (x, y) at  base + (y + E) * pitch + (x + XL)
+// Everything outside the owned rectangle is a halo: zero where it lies
+// outside the global domain (the reference's boundary() volume constraint,
+// src/2d_nonlocal_serial.cpp:213-221), filled from neighbouring blocks each
+// step otherwise.  The kernels therefore never test for the boundary.
+#pragma once
+#include <cstdint>
+
+namespace nlh {
+
+constexpr int kMaxRects = 16;
+constexpr int kMaxCopies = 64;
+
+// One output rectangle of a launch, in block-local node coordinates.
+struct Rect {
+  const double *u;    // node (0,0) of the current field
+  double *un;         // node (0,0) of the next field
+  const double *lw;   // node (0,0) of L_h[W0] (fast test mode) or nullptr
+  int64_t pitch;      // doubles per padded row
+  int32_t gx0, gy0;   // global coordinates of node (0,0)
+  int32_t x0, y0, x1, y1;
+  int32_t wg_begin;   // first work item of this rect
+  int32_t nstrip;     // fast kernel: strips of 64*R columns
+  int32_t nseg;       // fast kernel: segments of seg_h rows
+  int32_t pad_;
+};
+
+struct RectList {
+  Rect r[kMaxRects];
+  int32_t nrects;
+  int32_t nwork;
+};
+
+// Per-step constants.  All trig values are computed on the host with glibc
+// so that w() is bit-identical to the reference's.
+struct StepConst {
+  double c2d;      // (k*8)/pow(eps*dh,4)           reference :76
+  double dh2;      // dh*dh
+  double dt;
+  double alpha;    // c2d*dh2*dt            (fast kernel)
+  double nf;       // N(eps) as double      (fast kernel)
+  double st2pi;    // (2*pi)*sin(2*pi*(t*dt))
+  double ct;       // cos(2*pi*(t*dt))
+  const double *sxt;  // sin(2*pi*(g*dh)), g in [-E, nx+E), index g+E
+  const double *syt;  // same over y
+  const int32_t *lens;  // len_1d_line(|d|) for d in [0, E]
+  int64_t nx, ny;  // global lattice
+  int32_t E;
+  int32_t seg_h;   // fast kernel segment height
+};
+
+// Strided rectangle copy (halo exchange: local block->block copies, pack to
+// and unpack from RCCL message buffers).
+struct Copy {
+  const double *src;
+  double *dst;
+  int64_t spitch, dpitch;  // elements
+  int32_t w, h;
+  int32_t wg_begin;
+  int32_t pad_;
+};
+struct CopyList {
+  Copy c[kMaxCopies];
+  int32_t ncopies;
+  int32_t nwork;
+};
+
+struct NormPartial {
+  double l2;
+  double linf;
+};
+
+// ---- launch API (nlh_kernels.hip) -----------------------------------------
+// Returns false if (E, R) has no fast instantiation.
+bool fast_supported(int E);
+int fast_strip_width(int E);    // 64*R columns per strip
+int fast_seg_min(int E);        // smallest sensible segment height
+// Work-item counts are filled into rl by the caller (wg_begin/nwork).
+int launch_fast(const RectList &rl, const StepConst &c, bool test, void *stream);
+int launch_exact(const RectList &rl, const StepConst &c, bool test, void *stream);
+// A = sum_local(u) only (no time update) -- used once for L_h[W0].
+int launch_exact_sum(const RectList &rl, const StepConst &c, void *stream);
+int launch_copies(const CopyList &cl, void *stream);
+// u(x,y) = sxt[gx]*syt[gy] on the block interior; halo untouched.
+int launch_init_test(double *u, int64_t pitch, int32_t bx, int32_t by,
+                     int32_t gx0, int32_t gy0, const StepConst &c, void *stream);
+// W0 over the padded block INCLUDING halo: sxt*syt inside the domain, 0 out.
+int launch_fill_w0(double *u, int64_t pitch, int32_t xl, int32_t bx,
+                   int32_t by, int32_t gx0, int32_t gy0, const StepConst &c,
+                   void *stream);
+// Partial L2/Linf per workgroup into `out` (nwg entries); returns nwg.
+int norm_workgroups(int32_t bx, int32_t by);
+int launch_norms(const double *u, int64_t pitch, int32_t bx, int32_t by,
+                 int32_t gx0, int32_t gy0, const StepConst &c,
+                 NormPartial *out, void *stream);
+
+}  // namespace nlh

@@ -1,0 +1,57 @@
+// nlh_plan.h -- host-only decomposition of the lattice into per-rank blocks
+// and the per-step halo plan.  No device code; unit-tested on the CPU through
+// nlh_halo_plan()/nlh_resolve_owner().
+//
+// Reference behaviour replaced:
+//   tile ownership  locidx()              src/2d_nonlocal_distributed.cpp:105-110
+//   --file map      param_file_input()    src/2d_nonlocal_distributed.cpp:467-488
+//   neighbour set   add_neighbour_rectangle()  src/2d_nonlocal_distributed.cpp:982-992
+// The reference ships WHOLE neighbour tiles through HPX actions every step
+// (get_data_action, :1121-1131); here each rank holds its tiles merged into
+// rectangular blocks padded by an eps-wide halo, and only the halo
+// intersections move (RCCL send/recv between ranks, device copies within).
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace nlh {
+
+struct GRect {
+  int64_t x0 = 0, y0 = 0, w = 0, h = 0;
+  bool empty() const { return w <= 0 || h <= 0; }
+};
+
+GRect intersect(const GRect &a, const GRect &b);
+
+struct BlockDesc {
+  int32_t rank = 0;  // owner
+  int32_t local = 0; // index among the owner's blocks
+  GRect r;           // global node rectangle
+};
+
+struct Piece {
+  int32_t src_rank = 0, dst_rank = 0;
+  int32_t src_block = 0, dst_block = 0;  // indices into Plan::blocks
+  GRect r;                                // global rectangle
+};
+
+struct Plan {
+  std::vector<BlockDesc> blocks;  // ordered by (rank, local)
+  std::vector<Piece> pieces;      // ordered by (dst_block, src_block)
+};
+
+// owner_out[i] for tile i = gx + gy*tiles_x.  owner_in == nullptr selects the
+// reference default (i*nranks)/(tiles_x*tiles_y).  Returns false (and sets
+// err) for an owner out of [0, nranks).
+bool resolve_owner(int64_t tiles_x, int64_t tiles_y, int32_t nranks,
+                   const int32_t *owner_in, std::vector<int32_t> &owner_out,
+                   std::string &err);
+
+// Merge each rank's tiles into rectangles (maximal x-runs per tile row,
+// merged downwards when a run repeats) and build the halo pieces for a
+// horizon `eps`.
+Plan make_plan(int64_t nx, int64_t ny, int64_t eps, int64_t tiles_x,
+               int64_t tiles_y, const std::vector<int32_t> &owner);
+
+}  // namespace nlh
