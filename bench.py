@@ -1,0 +1,203 @@
+#!/usr/bin/env python3
+"""Benchmark of the explicit-Euler hot path (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+
+Workload (BASELINE.json configs[1]): a 4096 x 4096
+lattice PER GPU, eps = 8, fp64, production mode (test=0: the nonlocal
+operator only, as in the reference's non-test runs), synthetic test_init IC,
+k = 1, dh = 1/4096, dt = eps^4 dh^2 / (8 k N(eps)).  One "step" = one explicit
+Euler step of the whole lattice.  N > 1 GPUs: one process per GPU (launched by
+torch.distributed.run), the lattice grows with N (weak scaling) as a px x py
+block decomposition with eps-wide ghost strips exchanged over RCCL each step.
+
+Prints one JSON line (rank 0) with the roofline of the dominant kernel
+(HIP events on the stencil's own stream) and a bounded CPU baseline (the
+oracle's tiled 2d_nonlocal_async restatement on the host cores).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import nonlocalheatequation_amd as N  # noqa: E402
+
+EPS = 8
+NB = 4096                      # lattice per GPU (each direction)
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
+FP64_VEC_PEAK_TFLOPS = 78.6    # 256 CU x 64 lanes x 2 x 2.4 GHz (spec)
+BYTES_PER_NODE = 16.0          # read u once + write u' once
+
+
+def decomposition(n: int):
+    px = 1
+    while px * px < n:
+        px *= 2
+    while n % px:
+        px //= 2
+    return px, n // px
+
+
+def cpu_baseline(nthreads: int, budget_s: float = 12.0) -> dict:
+    """Oracle restatement of 2d_nonlocal_async (np x np tiles, one task per
+    tile per step, a barrier per step) on the same 4096^2 / eps=8 workload,
+    bounded to ~budget_s of CPU time."""
+    from oracle import oracle as O  # test infrastructure: baseline leg only
+
+    dh = 1.0 / NB
+    dt = EPS ** 4 * dh * dh / (8.0 * N.disk_count(EPS))
+    p = O.params(NB, NB, EPS, 1.0, dt, dh, 0)
+    u = O.test_init(p)
+    tiles = 32  # 128 x 128-node tiles
+    t1 = O.run_tiled(p, 1, tiles, tiles, u, nthreads)
+    steps = int(max(1, min(20, budget_s / max(t1, 1e-3) - 1)))
+    t = O.run_tiled(p, steps, tiles, tiles, u, nthreads)
+    rate = NB * NB * steps / t / 1e9
+    return {"value": rate, "unit": "Gnode-updates/s", "cores": nthreads, "kind": "port",
+            "sample": f"{NB}x{NB} lattice, eps={EPS}, test=0, {steps} step(s) after 1 warm-up step, "
+                      f"{tiles}x{tiles} tiles, oracle/nlh_oracle.c run_tiled (-O3 -ffp-contract=off)"}
+
+
+def read_traffic():
+    """HBM bytes per stencil launch from the committed rocprofv3 PMC summary
+    (FETCH_SIZE doubled per the gfx950 correction + WRITE_SIZE)."""
+    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--kernel", default="fast", choices=["fast", "exact"])
+    ap.add_argument("--seg-rows", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and world > 1:
+        print(f"--gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    nranks = world
+
+    dist = None
+    if nranks > 1:
+        import torch.distributed as dist  # control plane only (id broadcast, barrier, max)
+        dist.init_process_group("gloo")
+
+    px, py = decomposition(nranks)
+    nx, ny = NB * px, NB * py
+    dh = 1.0 / NB
+    dt = EPS ** 4 * dh * dh / (8.0 * N.disk_count(EPS))
+
+    comm_id = None
+    if nranks > 1:
+        obj = [N.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        comm_id = obj[0]
+
+    s = N.Solver(nx, ny, EPS, 1.0, dt, dh, test=False, kernel=args.kernel, device=local,
+                 rank=rank, nranks=nranks, tiles=(px, py), comm_id=comm_id, seg_rows=args.seg_rows)
+    s.test_init()
+    s.run(args.warmup)
+    s.synchronize()
+
+    def barrier():
+        s.synchronize()
+        if dist is not None:
+            dist.barrier()
+
+    # kernel-duration measurement (events on the stencil stream), separate pass
+    s.kernel_timing(True)
+    s.run(min(args.steps, 200))
+    s.synchronize()
+    k_ms, k_n = s.kernel_time()
+    s.kernel_timing(False)
+
+    barrier()
+    t0 = time.perf_counter()
+    s.run(args.steps)
+    s.synchronize()
+    t1 = time.perf_counter()
+    barrier()
+    elapsed = t1 - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    info = s.info()
+    total_nodes = nx * ny
+    value = total_nodes * args.steps / elapsed / 1e9
+    ms_per_step = elapsed * 1e3 / args.steps
+    local_nodes = info.owned_nodes
+    avg_launch_s = (k_ms / 1e3) / max(k_n, 1)
+    achieved_gbs = BYTES_PER_NODE * local_nodes / avg_launch_s / 1e9
+    fp64_equiv_tflops = 2.0 * info.disk_points * local_nodes / avg_launch_s / 1e12
+    traffic = read_traffic()
+
+    result = None
+    if rank == 0:
+        cpu = None
+        if not args.no_cpu_baseline and nranks == 1:
+            cpu = cpu_baseline(nthreads=min(16, os.cpu_count() or 1))
+        result = {
+            "metric": "Gnode-updates/s (nodes*steps/s) eps=8 fp64",
+            "value": value,
+            "unit": "Gnode-updates/s",
+            "n_gpus": nranks,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (test_init IC sin(2 pi x) sin(2 pi y); no dataset)",
+            "config": {
+                "workload": f"C2: {NB}x{NB} lattice per GPU, eps={EPS}, production step (test=0), "
+                            f"{args.kernel} kernel" + (f", {px}x{py} blocks + RCCL ghost exchange" if nranks > 1 else ""),
+                "lattice": [nx, ny], "eps": EPS, "blocks": [px, py],
+                "disk_points": info.disk_points, "dt": dt, "dh": dh, "kernel": args.kernel,
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved_gbs,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved_gbs / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "kernel_avg_us": avg_launch_s * 1e6,
+                "kernel_launches_timed": k_n,
+                "algorithmic_bytes_per_launch": BYTES_PER_NODE * local_nodes,
+                "fp64_direct_sum_equiv_tflops": fp64_equiv_tflops,
+                "fp64_direct_sum_equiv_frac": fp64_equiv_tflops / FP64_VEC_PEAK_TFLOPS,
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(result), flush=True)
+    s.close()
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
