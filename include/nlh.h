@@ -71,6 +71,9 @@ typedef struct nlh_params {
   int32_t rank;         /* this process, 0 <= rank < nranks                    */
   int32_t nranks;       /* processes (one per GPU); 1 = single GPU             */
   int32_t seg_rows;     /* FAST kernel segment height, 0 = automatic           */
+  int32_t split_tiles;  /* 1: one device block per tile (no merging of a rank's */
+                        /*   tiles into rectangles; exercises the halo path)  */
+  int32_t reserved_;    /* must be 0                                           */
   int64_t tiles_x;      /* tile grid over the lattice (reference npx / np);    */
   int64_t tiles_y;      /*   must divide nx / ny.  1x1 for the serial driver   */
   const int32_t *owner; /* tiles_x*tiles_y owner ranks, index gx + gy*tiles_x; */
@@ -95,6 +98,15 @@ int nlh_init_test(nlh_solver *s);
 int nlh_set_field(nlh_solver *s, const double *u_global);
 /* Copy the owned nodes of the current field into the global host array.   */
 int nlh_get_field(nlh_solver *s, double *u_global);
+
+/* Collective over all ranks (nranks > 1; plain copy when nranks == 1): the
+ * GLOBAL field at the current step into u_global on rank `root` (other
+ * ranks may pass NULL).  Used by the drivers' --cmp / --results / logging,
+ * which the reference serves by pulling every tile to locality 0
+ * (vector_get_data, src/2d_nonlocal_distributed.cpp:496,1121-1131).      */
+int nlh_gather_field(nlh_solver *s, int32_t root, double *u_global);
+/* Collective: returns once every rank has finished its enqueued steps.    */
+int nlh_barrier(nlh_solver *s);
 
 /* Advance `nsteps` explicit-Euler steps from the current step index.
  * Asynchronous: returns once the work is enqueued (nlh_synchronize waits). */
@@ -140,6 +152,11 @@ int nlh_resolve_owner(int64_t tiles_x, int64_t tiles_y, int32_t nranks,
  * (a global rectangle copied from the owner's interior into the halo of
  * block dst_block of dst_rank).                                           */
 int64_t nlh_halo_plan(const nlh_params *p, int64_t *pieces, int64_t cap);
+
+/* Host-only block plan: number of device blocks over ALL ranks and, if
+ * `blocks` is non-NULL, up to `cap` records of 6 int64 each:
+ *   {rank, local_index, gx0, gy0, w, h}                                    */
+int64_t nlh_block_plan(const nlh_params *p, int64_t *blocks, int64_t cap);
 
 const char *nlh_last_error(void);
 int nlh_abi_version(void);

@@ -27,7 +27,7 @@ import numpy as np
 
 __all__ = [
     "KERNEL_AUTO", "KERNEL_EXACT", "KERNEL_FAST", "NLHError", "Solver",
-    "lib", "lib_path", "comm_unique_id", "resolve_owner", "halo_plan",
+    "lib", "lib_path", "comm_unique_id", "resolve_owner", "halo_plan", "block_plan",
     "disk_count", "batch_tester", "BatchRow",
 ]
 
@@ -51,6 +51,7 @@ class _Params(ctypes.Structure):
         ("k", ctypes.c_double), ("dt", ctypes.c_double), ("dh", ctypes.c_double),
         ("test", ctypes.c_int32), ("kernel", ctypes.c_int32), ("device", ctypes.c_int32),
         ("rank", ctypes.c_int32), ("nranks", ctypes.c_int32), ("seg_rows", ctypes.c_int32),
+        ("split_tiles", ctypes.c_int32), ("reserved_", ctypes.c_int32),
         ("tiles_x", ctypes.c_int64), ("tiles_y", ctypes.c_int64),
         ("owner", ctypes.POINTER(ctypes.c_int32)),
         ("comm_id", ctypes.POINTER(ctypes.c_uint8)),
@@ -77,6 +78,8 @@ _SIGNATURES = {
     "nlh_set_field": ([ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
     "nlh_get_field": ([ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
     "nlh_run": ([ctypes.c_void_p, ctypes.c_int64], ctypes.c_int),
+    "nlh_gather_field": ([ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
+    "nlh_barrier": ([ctypes.c_void_p], ctypes.c_int),
     "nlh_synchronize": ([ctypes.c_void_p], ctypes.c_int),
     "nlh_step_index": ([ctypes.c_void_p], ctypes.c_int64),
     "nlh_errors": ([ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_double),
@@ -89,6 +92,8 @@ _SIGNATURES = {
                            ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
     "nlh_halo_plan": ([ctypes.POINTER(_Params), ctypes.POINTER(ctypes.c_int64), ctypes.c_int64],
                       ctypes.c_int64),
+    "nlh_block_plan": ([ctypes.POINTER(_Params), ctypes.POINTER(ctypes.c_int64), ctypes.c_int64],
+                       ctypes.c_int64),
 }
 
 _lib = None
@@ -139,7 +144,7 @@ def resolve_owner(tiles_x: int, tiles_y: int, nranks: int, owner=None) -> np.nda
 
 
 def _make_params(nx, ny, eps, k, dt, dh, test, kernel, device, rank, nranks, seg_rows,
-                 tiles, owner, comm_id):
+                 tiles, owner, comm_id, split_tiles=False):
     p = _Params()
     p.nx, p.ny, p.eps = int(nx), int(ny), int(eps)
     p.k, p.dt, p.dh = float(k), float(dt), float(dh)
@@ -147,6 +152,7 @@ def _make_params(nx, ny, eps, k, dt, dh, test, kernel, device, rank, nranks, seg
     p.kernel = _KERNEL_NAMES[kernel] if isinstance(kernel, str) else int(kernel)
     p.device, p.rank, p.nranks, p.seg_rows = int(device), int(rank), int(nranks), int(seg_rows)
     p.tiles_x, p.tiles_y = int(tiles[0]), int(tiles[1])
+    p.split_tiles = int(bool(split_tiles))
     keep = []
     if owner is not None:
         o = np.ascontiguousarray(owner, dtype=np.int32)
@@ -159,11 +165,26 @@ def _make_params(nx, ny, eps, k, dt, dh, test, kernel, device, rank, nranks, seg
     return p, keep
 
 
-def halo_plan(nx, ny, eps, tiles=(1, 1), owner=None, rank=0, nranks=1) -> np.ndarray:
+def block_plan(nx, ny, eps, tiles=(1, 1), owner=None, nranks=1, split_tiles=False) -> np.ndarray:
+    """Host-only block plan over all ranks: (n, 6) int64 rows
+    {rank, local_index, gx0, gy0, w, h}."""
+    p, keep = _make_params(nx, ny, eps, 1.0, 1.0, 1.0, 0, KERNEL_AUTO, -1, 0, nranks, 0,
+                           tiles, owner, None, split_tiles)
+    n = lib().nlh_block_plan(ctypes.byref(p), None, 0)
+    if n < 0:
+        _check(int(-n), "nlh_block_plan")
+    out = np.zeros((max(n, 0), 6), dtype=np.int64)
+    if n > 0:
+        lib().nlh_block_plan(ctypes.byref(p), out.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), n)
+    del keep
+    return out
+
+
+def halo_plan(nx, ny, eps, tiles=(1, 1), owner=None, rank=0, nranks=1, split_tiles=False) -> np.ndarray:
     """Host-only halo plan: (n, 8) int64 rows
     {src_rank, dst_rank, gx0, gy0, w, h, src_block, dst_block} received by `rank`."""
     p, keep = _make_params(nx, ny, eps, 1.0, 1.0, 1.0, 0, KERNEL_AUTO, -1, rank, nranks, 0,
-                           tiles, owner, None)
+                           tiles, owner, None, split_tiles)
     n = lib().nlh_halo_plan(ctypes.byref(p), None, 0)
     if n < 0:
         _check(int(-n), "nlh_halo_plan")
@@ -205,14 +226,15 @@ class Solver:
     """
 
     def __init__(self, nx, ny, eps, k=1.0, dt=0.0005, dh=0.02, *, test=False, kernel="auto",
-                 device=-1, rank=0, nranks=1, tiles=(1, 1), owner=None, comm_id=None, seg_rows=0):
+                 device=-1, rank=0, nranks=1, tiles=(1, 1), owner=None, comm_id=None, seg_rows=0,
+                 split_tiles=False):
         self.nx, self.ny, self.eps = int(nx), int(ny), int(eps)
         self.k, self.dt, self.dh = float(k), float(dt), float(dh)
         self.test = bool(test)
         self.error_l2 = 0.0
         self.error_linf = 0.0
         p, keep = _make_params(nx, ny, eps, k, dt, dh, test, kernel, device, rank, nranks,
-                               seg_rows, tiles, owner, comm_id)
+                               seg_rows, tiles, owner, comm_id, split_tiles)
         h = ctypes.c_void_p()
         _check(lib().nlh_create(ctypes.byref(p), ctypes.byref(h)), "nlh_create")
         del keep
@@ -283,6 +305,15 @@ class Solver:
             out = np.zeros((self.ny, self.nx), dtype=np.float64)
         _check(lib().nlh_get_field(self._h, _dp(out)), "nlh_get_field")
         return out
+
+    def gather(self, root: int = 0) -> np.ndarray | None:
+        """Collective: the global field on rank `root` (None elsewhere)."""
+        out = np.zeros((self.ny, self.nx), dtype=np.float64)
+        _check(lib().nlh_gather_field(self._h, int(root), _dp(out)), "nlh_gather_field")
+        return out
+
+    def barrier(self) -> None:
+        _check(lib().nlh_barrier(self._h), "nlh_barrier")
 
     @property
     def step_index(self) -> int:

@@ -1,0 +1,329 @@
+// driver_common.cpp -- see driver_common.h.
+#include "driver_common.h"
+
+#include <arpa/inet.h>
+#include <netdb.h>
+#include <netinet/in.h>
+#include <sys/socket.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <ctime>
+#include <fstream>
+#include <iostream>
+#include <thread>
+
+#include "vtu_writer.h"
+
+namespace nlh_drv {
+
+// ---------------------------------------------------------------- options
+void Options::flag(const std::string &name) { flags_[name] = false; }
+
+void Options::opt(const std::string &name, const std::string &def) { vals_[name] = def; }
+
+bool Options::parse(int argc, char **argv, std::string &err) {
+  for (int i = 1; i < argc; ++i) {
+    std::string a = argv[i];
+    if (a.rfind("--hpx:", 0) == 0) {  // HPX runtime options: accepted, ignored
+      if (a.find('=') == std::string::npos && i + 1 < argc && argv[i + 1][0] != '-') ++i;
+      continue;
+    }
+    if (a.rfind("--", 0) != 0) {
+      err = "unexpected argument '" + a + "'";
+      return false;
+    }
+    std::string name = a.substr(2), val;
+    bool has_val = false;
+    const size_t eq = name.find('=');
+    if (eq != std::string::npos) {
+      val = name.substr(eq + 1);
+      name = name.substr(0, eq);
+      has_val = true;
+    }
+    if (flags_.count(name)) {
+      flags_[name] = true;
+      continue;
+    }
+    if (!vals_.count(name)) {
+      err = "unrecognised option '--" + name + "'";
+      return false;
+    }
+    if (!has_val) {
+      if (i + 1 >= argc) {
+        err = "the required argument for option '--" + name + "' is missing";
+        return false;
+      }
+      val = argv[++i];
+    }
+    vals_[name] = val;
+  }
+  return true;
+}
+
+bool Options::count(const std::string &name) const {
+  auto it = flags_.find(name);
+  return it != flags_.end() && it->second;
+}
+
+std::string Options::str(const std::string &name) const { return vals_.at(name); }
+
+bool Options::as_bool(const std::string &name) const {
+  std::string v = vals_.at(name);
+  std::transform(v.begin(), v.end(), v.begin(), ::tolower);
+  return v == "1" || v == "true" || v == "yes" || v == "on";
+}
+
+int64_t Options::as_i64(const std::string &name) const { return std::stoll(vals_.at(name)); }
+
+uint64_t Options::as_u64(const std::string &name) const { return std::stoull(vals_.at(name)); }
+
+double Options::as_double(const std::string &name) const { return std::stod(vals_.at(name)); }
+
+// ---------------------------------------------------------------- output
+void print_banner(const char *argv0) {
+  // MAJOR.MINOR.UPDATE of include/Config.h (0.1.0)
+  std::cout << argv0 << " (0.1.0)" << std::endl;
+}
+
+void print_time_results(uint64_t threads, uint64_t elapsed_ns, uint64_t nx, uint64_t ny,
+                        uint64_t nt, bool header) {
+  if (header)
+    std::cout << "OS_Threads,       Execution_Time_sec,"
+                 "       x dimension,        y dimension,        Time_Steps\n"
+              << std::flush;
+  const std::string t = std::to_string(threads) + ",", x = std::to_string(nx) + ",",
+                    y = std::to_string(ny) + ",", n = std::to_string(nt) + " ";
+  std::printf("%-21s %10.12lf,        %-21s %-21s %-21s\n", t.c_str(), elapsed_ns / 1e9, x.c_str(),
+              y.c_str(), n.c_str());
+  std::fflush(stdout);
+}
+
+void print_time_results(uint32_t localities, uint64_t threads, uint64_t elapsed_ns, uint64_t nx,
+                        uint64_t ny, uint64_t npx, uint64_t npy, uint64_t nt, bool header) {
+  if (header)
+    std::cout << "Localities,OS_Threads,Execution_Time_sec,"
+                 "       nx,    ny,     npx,    npy,    Time_Steps\n"
+              << std::flush;
+  const std::string l = std::to_string(localities) + ",", t = std::to_string(threads) + ",",
+                    x = std::to_string(nx) + ",", y = std::to_string(ny) + ",",
+                    px = std::to_string(npx) + ",", py = std::to_string(npy) + ",",
+                    n = std::to_string(nt) + " ";
+  std::printf("%-6s %-6s %.14g, %-21s %-21s %-21s %-21s %-21s\n", l.c_str(), t.c_str(),
+              elapsed_ns / 1e9, x.c_str(), y.c_str(), px.c_str(), py.c_str(), n.c_str());
+  std::fflush(stdout);
+}
+
+void print_errors(double l2, double linf) {
+  std::cout << "l2: " << l2 << " linfinity: " << linf << std::endl;
+}
+
+uint64_t now_ns() {
+  return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+// ---------------------------------------------------------------- ranks
+static int env_int(const char *a, int def) {
+  const char *v = std::getenv(a);
+  return v ? std::atoi(v) : def;
+}
+
+RankEnv rank_env() {
+  RankEnv r;
+  const char *sets[][3] = {{"RANK", "WORLD_SIZE", "LOCAL_RANK"},
+                           {"OMPI_COMM_WORLD_RANK", "OMPI_COMM_WORLD_SIZE", "OMPI_COMM_WORLD_LOCAL_RANK"},
+                           {"SLURM_PROCID", "SLURM_NTASKS", "SLURM_LOCALID"},
+                           {"PMI_RANK", "PMI_SIZE", "MPI_LOCALRANKID"}};
+  for (auto &s : sets) {
+    if (std::getenv(s[0]) && std::getenv(s[1])) {
+      r.rank = env_int(s[0], 0);
+      r.nranks = env_int(s[1], 1);
+      r.local_rank = env_int(s[2], r.rank);
+      break;
+    }
+  }
+  return r;
+}
+
+static bool send_all(int fd, const void *p, size_t n) {
+  const char *c = (const char *)p;
+  while (n) {
+    const ssize_t k = ::send(fd, c, n, 0);
+    if (k <= 0) return false;
+    c += k;
+    n -= (size_t)k;
+  }
+  return true;
+}
+
+static bool recv_all(int fd, void *p, size_t n) {
+  char *c = (char *)p;
+  while (n) {
+    const ssize_t k = ::recv(fd, c, n, 0);
+    if (k <= 0) return false;
+    c += k;
+    n -= (size_t)k;
+  }
+  return true;
+}
+
+bool share_comm_id(const RankEnv &re, uint8_t id[NLH_COMM_ID_BYTES], std::string &err) {
+  const char *addr = std::getenv("MASTER_ADDR");
+  const int port = env_int("MASTER_PORT", 29517) + 1;  // next to torch's own store port
+  if (!addr) addr = "127.0.0.1";
+  if (re.rank == 0) {
+    if (nlh_comm_unique_id(id) != NLH_OK) {
+      err = nlh_last_error();
+      return false;
+    }
+    const int lfd = ::socket(AF_INET, SOCK_STREAM, 0);
+    int one = 1;
+    ::setsockopt(lfd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+    sockaddr_in sa{};
+    sa.sin_family = AF_INET;
+    sa.sin_port = htons((uint16_t)port);
+    sa.sin_addr.s_addr = htonl(INADDR_ANY);
+    if (::bind(lfd, (sockaddr *)&sa, sizeof(sa)) != 0 || ::listen(lfd, re.nranks) != 0) {
+      err = "cannot listen on port " + std::to_string(port);
+      ::close(lfd);
+      return false;
+    }
+    for (int i = 1; i < re.nranks; ++i) {
+      const int fd = ::accept(lfd, nullptr, nullptr);
+      if (fd < 0 || !send_all(fd, id, NLH_COMM_ID_BYTES)) {
+        err = "bootstrap accept/send failed";
+        ::close(lfd);
+        return false;
+      }
+      ::close(fd);
+    }
+    ::close(lfd);
+    return true;
+  }
+  addrinfo hints{}, *res = nullptr;
+  hints.ai_family = AF_INET;
+  hints.ai_socktype = SOCK_STREAM;
+  if (::getaddrinfo(addr, std::to_string(port).c_str(), &hints, &res) != 0 || !res) {
+    err = std::string("cannot resolve MASTER_ADDR ") + addr;
+    return false;
+  }
+  bool ok = false;
+  for (int attempt = 0; attempt < 600 && !ok; ++attempt) {  // up to ~60 s
+    const int fd = ::socket(AF_INET, SOCK_STREAM, 0);
+    if (::connect(fd, res->ai_addr, res->ai_addrlen) == 0) ok = recv_all(fd, id, NLH_COMM_ID_BYTES);
+    ::close(fd);
+    if (!ok) std::this_thread::sleep_for(std::chrono::milliseconds(100));
+  }
+  ::freeaddrinfo(res);
+  if (!ok) err = "bootstrap: could not fetch the RCCL id from rank 0";
+  return ok;
+}
+
+int kernel_from_name(const std::string &s) {
+  if (s == "exact") return NLH_KERNEL_EXACT;
+  if (s == "fast") return NLH_KERNEL_FAST;
+  return NLH_KERNEL_AUTO;
+}
+
+double w_exact(int64_t x, int64_t y, int64_t t, double dt, double dh) {
+  return cos(2 * M_PI * (t * dt)) * sin(2 * M_PI * (x * dh)) * sin(2 * M_PI * (y * dh));
+}
+
+// ---------------------------------------------------------------- logging
+static bool is_dir(const std::string &p) {
+  struct stat st;
+  return ::stat(p.c_str(), &st) == 0 && S_ISDIR(st.st_mode);
+}
+
+void Logger::probe() {
+  csv_ok = is_dir(csv_dir);
+  vtk_ok = is_dir(vtk_dir);
+}
+
+void Logger::log(int64_t t, int64_t vtk_index, const std::vector<double> &u) {
+  if (vtk_ok) {
+    VtuWriter v(vtk_dir + "/simulate_" + std::to_string(vtk_index));
+    v.append_lattice_nodes(nx, ny);
+    v.append_point_data("Temperature", u);
+    v.add_time_step((double)std::time(nullptr));
+    v.close();
+  }
+  if (!csv_ok) return;
+  std::ofstream out(csv_dir + "/simulate_2d.csv", std::ios_base::app);
+  std::vector<double> sx(nx), sy(ny);
+  const double ct = cos(2 * M_PI * (t * dt));
+  for (int64_t x = 0; x < nx; ++x) sx[x] = sin(2 * M_PI * (x * dh));
+  for (int64_t y = 0; y < ny; ++y) sy[y] = sin(2 * M_PI * (y * dh));
+  double l2 = 0, linf = 0;
+  for (int64_t x = 0; x < nx; ++x)
+    for (int64_t y = 0; y < ny; ++y) {
+      const double uu = u[x + y * nx], w = ct * sx[x] * sy[y];
+      out << t << "," << x << "," << y << "," << uu << "," << w << "," << (uu - w) * (uu - w) << ","
+          << std::abs(uu - w) << ",\n";
+      l2 += (uu - w) * (uu - w);
+      linf = std::max(std::abs(uu - w), linf);
+    }
+  out.close();
+  if (test) {
+    std::ofstream sc(csv_dir + "/score_2d.csv", std::ios_base::app);
+    sc << t << "," << l2 << "," << linf << ",\n";
+  }
+}
+
+// ---------------------------------------------------------------- loop
+int run_steps(nlh_solver *s, int64_t nt, int64_t nlog, Logger &lg, bool vtk_index_is_t,
+              int rank, uint64_t &elapsed_ns) {
+  const bool logging = lg.enabled() && nlog > 0;
+  std::vector<double> u;
+  if (logging) u.assign((size_t)(lg.nx * lg.ny), 0.0);
+  int rc = nlh_barrier(s);
+  if (rc) return rc;
+  const uint64_t t0 = now_ns();
+  int64_t t = 0;
+  while (t < nt) {
+    int64_t last = nt - 1;  // last step of this chunk
+    if (logging) {
+      const int64_t next_log = (t % nlog == 0) ? t : (t / nlog + 1) * nlog;
+      last = std::min(last, next_log);
+    }
+    if ((rc = nlh_run(s, last - t + 1)) != NLH_OK) return rc;
+    t = last + 1;
+    if (logging && last % nlog == 0) {
+      if ((rc = nlh_gather_field(s, 0, rank == 0 ? u.data() : nullptr)) != NLH_OK) return rc;
+      if (rank == 0) lg.log(last, vtk_index_is_t ? last : last / nlog, u);
+    }
+  }
+  if ((rc = nlh_barrier(s)) != NLH_OK) return rc;
+  elapsed_ns = now_ns() - t0;
+  return NLH_OK;
+}
+
+bool read_partition_file(const std::string &path, int64_t &nx, int64_t &ny, int64_t &npx,
+                         int64_t &npy, double &dh, std::vector<int32_t> &owner) {
+  std::ifstream in(path);
+  if (!in) return false;
+  in >> nx >> ny >> npx >> npy >> dh;
+  owner.assign((size_t)(npx * npy), 0);
+  for (int64_t ix = 0; ix < npx; ++ix)
+    for (int64_t iy = 0; iy < npy; ++iy) {
+      int64_t px = 0, py = 0, loc = 0;
+      in >> px >> py >> loc;
+      if (px >= 0 && px < npx && py >= 0 && py < npy) owner[(size_t)(px + py * npx)] = (int32_t)loc;
+    }
+  return true;
+}
+
+int die(const char *what) {
+  std::cerr << what << ": " << nlh_last_error() << std::endl;
+  return 1;
+}
+
+}  // namespace nlh_drv

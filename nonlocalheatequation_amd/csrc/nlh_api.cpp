@@ -92,11 +92,12 @@ struct nlh_solver {
   nlh::StepConst sc{};
   int64_t disk = 0;
   bool exchange = false;
-  nlh::RectList rl_full[2]{}, rl_int[2]{}, rl_bnd[2]{};
+  // launches per phase and parity (chunked at kMaxRects / kMaxCopies)
+  std::vector<nlh::RectList> rl_full[2], rl_int[2], rl_bnd[2];
   // halo exchange
   ncclComm_t comm = nullptr;
   std::vector<Peer> peers;
-  nlh::CopyList cl_pack[2]{}, cl_unpack[2]{}, cl_local[2]{};
+  std::vector<nlh::CopyList> cl_pack[2], cl_unpack[2], cl_local[2];
   int64_t halo_bytes = 0;
   // norms
   nlh::NormPartial *d_part = nullptr;
@@ -178,13 +179,17 @@ int build_rectlists(nlh_solver *s) {
                               : (int)std::max<int64_t>(nlh::fast_seg_min(E), ceil_div(strip_rows, 2048));
   }
   s->sc.seg_h = seg_h;
-  auto make = [&](const std::vector<Item> &items, int k, nlh::RectList &rl) -> int {
-    std::memset(&rl, 0, sizeof(rl));
-    // when not exchanging, one launch covers every rect of every block
+  auto make = [&](const std::vector<Item> &items, int k, std::vector<nlh::RectList> &out) -> int {
+    out.clear();
     int w = 0;
     for (auto &it : items) {
-      if (rl.nrects >= nlh::kMaxRects)
-        return fail(NLH_ERR_UNSUPPORTED, "too many output rectangles on this rank");
+      if (out.empty() || out.back().nrects >= nlh::kMaxRects) {
+        if (!out.empty()) out.back().nwork = w;
+        out.emplace_back();
+        std::memset(&out.back(), 0, sizeof(nlh::RectList));
+        w = 0;
+      }
+      nlh::RectList &rl = out.back();
       nlh::Rect &R = rl.r[rl.nrects++];
       fill_rect_common(R, s->blocks[it.blk], k, s);
       R.x0 = it.r.x0; R.y0 = it.r.y0; R.x1 = it.r.x1; R.y1 = it.r.y1;
@@ -198,7 +203,7 @@ int build_rectlists(nlh_solver *s) {
       R.wg_begin = w;
       w += R.nstrip * R.nseg;
     }
-    rl.nwork = w;
+    if (!out.empty()) out.back().nwork = w;
     return NLH_OK;
   };
   for (int k = 0; k < 2; ++k) {
@@ -210,11 +215,14 @@ int build_rectlists(nlh_solver *s) {
   return NLH_OK;
 }
 
-int add_copy(nlh::CopyList &cl, const double *src, int64_t spitch, double *dst,
+int add_copy(std::vector<nlh::CopyList> &v, const double *src, int64_t spitch, double *dst,
              int64_t dpitch, int64_t w, int64_t h) {
   if (w <= 0 || h <= 0) return NLH_OK;
-  if (cl.ncopies >= nlh::kMaxCopies)
-    return fail(NLH_ERR_UNSUPPORTED, "too many halo pieces on this rank");
+  if (v.empty() || v.back().ncopies >= nlh::kMaxCopies) {
+    v.emplace_back();
+    std::memset(&v.back(), 0, sizeof(nlh::CopyList));
+  }
+  nlh::CopyList &cl = v.back();
   nlh::Copy &c = cl.c[cl.ncopies++];
   c.src = src;
   c.dst = dst;
@@ -252,10 +260,10 @@ int build_exchange(nlh_solver *s) {
   }
   for (int k = 0; k < 2; ++k) {
     std::map<int, int64_t> soff, roff;
-    nlh::CopyList &pk = s->cl_pack[k], &up = s->cl_unpack[k], &lc = s->cl_local[k];
-    std::memset(&pk, 0, sizeof(pk));
-    std::memset(&up, 0, sizeof(up));
-    std::memset(&lc, 0, sizeof(lc));
+    auto &pk = s->cl_pack[k], &up = s->cl_unpack[k], &lc = s->cl_local[k];
+    pk.clear();
+    up.clear();
+    lc.clear();
     for (auto &pc : s->plan.pieces) {
       const int64_t n = pc.r.w * pc.r.h;
       int rc = NLH_OK;
@@ -294,15 +302,23 @@ hipEvent_t pool_event(nlh_solver *s) {
   return s->ev_pool[s->ev_used++];
 }
 
-int launch_stencil(nlh_solver *s, const nlh::RectList &rl) {
-  if (rl.nwork == 0) return NLH_OK;
-  int rc;
+int launch_stencil(nlh_solver *s, const std::vector<nlh::RectList> &v) {
   const bool test = s->p.test != 0;
-  if (s->kernel == NLH_KERNEL_FAST)
-    rc = nlh::launch_fast(rl, s->sc, test, s->s_main);
-  else
-    rc = nlh::launch_exact(rl, s->sc, test, s->s_main);
-  if (rc != 0) return fail(NLH_ERR_HIP, std::string("stencil launch failed: ") + hipGetErrorString((hipError_t)rc));
+  for (const auto &rl : v) {
+    if (rl.nwork == 0) continue;
+    int rc;
+    if (s->kernel == NLH_KERNEL_FAST)
+      rc = nlh::launch_fast(rl, s->sc, test, s->s_main);
+    else
+      rc = nlh::launch_exact(rl, s->sc, test, s->s_main);
+    if (rc != 0) return fail(NLH_ERR_HIP, std::string("stencil launch failed: ") + hipGetErrorString((hipError_t)rc));
+  }
+  return NLH_OK;
+}
+
+int launch_copy_lists(const std::vector<nlh::CopyList> &v, hipStream_t st) {
+  for (const auto &cl : v)
+    if (nlh::launch_copies(cl, st)) return fail(NLH_ERR_HIP, "halo copy launch");
   return NLH_OK;
 }
 
@@ -330,7 +346,7 @@ int enqueue_step(nlh_solver *s) {
   } else {
     HIP_TRY(hipEventRecord(s->ev_ready, s->s_main));
     HIP_TRY(hipStreamWaitEvent(s->s_comm, s->ev_ready, 0));
-    if (nlh::launch_copies(s->cl_pack[k], s->s_comm)) return fail(NLH_ERR_HIP, "pack launch");
+    if (launch_copy_lists(s->cl_pack[k], s->s_comm)) return NLH_ERR_HIP;
     if (!s->peers.empty()) {
       NCCL_TRY(ncclGroupStart());
       for (auto &pr : s->peers) {
@@ -339,8 +355,8 @@ int enqueue_step(nlh_solver *s) {
       }
       NCCL_TRY(ncclGroupEnd());
     }
-    if (nlh::launch_copies(s->cl_unpack[k], s->s_comm)) return fail(NLH_ERR_HIP, "unpack launch");
-    if (nlh::launch_copies(s->cl_local[k], s->s_comm)) return fail(NLH_ERR_HIP, "local halo launch");
+    if (launch_copy_lists(s->cl_unpack[k], s->s_comm)) return NLH_ERR_HIP;
+    if (launch_copy_lists(s->cl_local[k], s->s_comm)) return NLH_ERR_HIP;
     HIP_TRY(hipEventRecord(s->ev_halo, s->s_comm));
     if (e0) HIP_TRY(hipEventRecord(e0, s->s_main));
     int rc = launch_stencil(s, s->rl_int[k]);
@@ -429,7 +445,7 @@ int create_impl(const nlh_params *pin, nlh_solver *s) {
 
   std::string err;
   if (!nlh::resolve_owner(tx, ty, p.nranks, p.owner, s->owner, err)) return fail(NLH_ERR_ARG, err);
-  s->plan = nlh::make_plan(p.nx, p.ny, p.eps, tx, ty, s->owner);
+  s->plan = nlh::make_plan(p.nx, p.ny, p.eps, tx, ty, s->owner, p.split_tiles == 0);
 
   // ---- device
   int ndev = 0;
@@ -519,8 +535,6 @@ int create_impl(const nlh_params *pin, nlh_solver *s) {
     }
     s->blocks.push_back(b);
   }
-  if (s->blocks.size() > (size_t)nlh::kMaxRects)
-    return fail(NLH_ERR_UNSUPPORTED, "too many blocks on one rank");
 
   int rc = build_rectlists(s);
   if (rc) return rc;
@@ -628,6 +642,78 @@ int nlh_get_field(nlh_solver *s, double *u) {
     HIP_TRY(hipMemcpy2D(u + b.r.y0 * s->p.nx + b.r.x0, s->p.nx * sizeof(double), b.origin(s->cur),
                         b.pitch * sizeof(double), b.r.w * sizeof(double), b.r.h,
                         hipMemcpyDeviceToHost));
+  return NLH_OK;
+}
+
+int nlh_gather_field(nlh_solver *s, int32_t root, double *u) {
+  if (!s) return fail(NLH_ERR_ARG, "null solver");
+  if (root < 0 || root >= s->p.nranks) return fail(NLH_ERR_ARG, "bad root");
+  if (s->p.rank == root && !u) return fail(NLH_ERR_ARG, "root needs an output array");
+  int rc = set_device(s);
+  if (rc) return rc;
+  if (s->p.rank == root) {
+    rc = nlh_get_field(s, u);
+    if (rc) return rc;
+  }
+  if (!s->comm) return NLH_OK;
+  HIP_TRY(hipStreamSynchronize(s->s_main));
+  // every non-root rank ships its blocks, packed in plan order
+  std::vector<int64_t> count(s->p.nranks, 0);
+  for (auto &b : s->plan.blocks) count[b.rank] += b.r.w * b.r.h;
+  double *buf = nullptr;
+  int64_t maxc = 1;
+  for (int r = 0; r < s->p.nranks; ++r) maxc = std::max(maxc, count[r]);
+  HIP_TRY(hipMalloc(&buf, maxc * sizeof(double)));
+  int status = NLH_OK;
+  if (s->p.rank != root) {
+    int64_t off = 0;
+    for (auto &b : s->blocks) {
+      if (hipMemcpy2DAsync(buf + off, b.r.w * sizeof(double), b.origin(s->cur), b.pitch * sizeof(double),
+                           b.r.w * sizeof(double), b.r.h, hipMemcpyDeviceToDevice, s->s_comm) != hipSuccess)
+        status = fail(NLH_ERR_HIP, "gather pack");
+      off += b.r.w * b.r.h;
+    }
+    if (status == NLH_OK && count[s->p.rank] &&
+        ncclSend(buf, count[s->p.rank], ncclDouble, root, s->comm, s->s_comm) != ncclSuccess)
+      status = fail(NLH_ERR_RCCL, "gather send");
+    if (hipStreamSynchronize(s->s_comm) != hipSuccess && status == NLH_OK)
+      status = fail(NLH_ERR_HIP, "gather sync");
+  } else {
+    std::vector<double> h(maxc);
+    for (int r = 0; r < s->p.nranks && status == NLH_OK; ++r) {
+      if (r == root || !count[r]) continue;
+      if (ncclRecv(buf, count[r], ncclDouble, r, s->comm, s->s_comm) != ncclSuccess) {
+        status = fail(NLH_ERR_RCCL, "gather recv");
+        break;
+      }
+      if (hipMemcpyAsync(h.data(), buf, count[r] * sizeof(double), hipMemcpyDeviceToHost, s->s_comm) != hipSuccess ||
+          hipStreamSynchronize(s->s_comm) != hipSuccess) {
+        status = fail(NLH_ERR_HIP, "gather copy");
+        break;
+      }
+      int64_t off = 0;
+      for (auto &b : s->plan.blocks) {
+        if (b.rank != r) continue;
+        for (int64_t y = 0; y < b.r.h; ++y)
+          std::memcpy(u + (b.r.y0 + y) * s->p.nx + b.r.x0, h.data() + off + y * b.r.w, b.r.w * sizeof(double));
+        off += b.r.w * b.r.h;
+      }
+    }
+  }
+  (void)hipFree(buf);
+  return status;
+}
+
+int nlh_barrier(nlh_solver *s) {
+  if (!s) return fail(NLH_ERR_ARG, "null solver");
+  int rc = set_device(s);
+  if (rc) return rc;
+  HIP_TRY(hipStreamSynchronize(s->s_main));
+  HIP_TRY(hipStreamSynchronize(s->s_comm));
+  if (s->comm) {
+    NCCL_TRY(ncclAllReduce(s->d_red, s->d_red, 1, ncclDouble, ncclSum, s->comm, s->s_comm));
+    HIP_TRY(hipStreamSynchronize(s->s_comm));
+  }
   return NLH_OK;
 }
 
@@ -755,7 +841,7 @@ int64_t nlh_halo_plan(const nlh_params *p, int64_t *pieces, int64_t cap) {
   std::vector<int32_t> o;
   std::string err;
   if (!nlh::resolve_owner(tx, ty, p->nranks, p->owner, o, err)) return -fail(NLH_ERR_ARG, err);
-  nlh::Plan plan = nlh::make_plan(p->nx, p->ny, p->eps, tx, ty, o);
+  nlh::Plan plan = nlh::make_plan(p->nx, p->ny, p->eps, tx, ty, o, p->split_tiles == 0);
   int64_t n = 0;
   for (auto &pc : plan.pieces) {
     if (pc.dst_rank != p->rank) continue;
@@ -769,6 +855,31 @@ int64_t nlh_halo_plan(const nlh_params *p, int64_t *pieces, int64_t cap) {
       r[5] = pc.r.h;
       r[6] = pc.src_block;
       r[7] = pc.dst_block;
+    }
+    ++n;
+  }
+  return n;
+}
+
+int64_t nlh_block_plan(const nlh_params *p, int64_t *blocks, int64_t cap) {
+  if (!p) return -fail(NLH_ERR_ARG, "null params");
+  const int64_t tx = p->tiles_x > 0 ? p->tiles_x : 1, ty = p->tiles_y > 0 ? p->tiles_y : 1;
+  if (p->nx <= 0 || p->ny <= 0 || p->nx % tx || p->ny % ty || p->nranks < 1)
+    return -fail(NLH_ERR_ARG, "bad lattice / tile grid");
+  std::vector<int32_t> o;
+  std::string err;
+  if (!nlh::resolve_owner(tx, ty, p->nranks, p->owner, o, err)) return -fail(NLH_ERR_ARG, err);
+  nlh::Plan plan = nlh::make_plan(p->nx, p->ny, p->eps, tx, ty, o, p->split_tiles == 0);
+  int64_t n = 0;
+  for (auto &b : plan.blocks) {
+    if (blocks && n < cap) {
+      int64_t *r = blocks + 6 * n;
+      r[0] = b.rank;
+      r[1] = b.local;
+      r[2] = b.r.x0;
+      r[3] = b.r.y0;
+      r[4] = b.r.w;
+      r[5] = b.r.h;
     }
     ++n;
   }

@@ -14,7 +14,7 @@
 
 namespace nlh {
 
-constexpr int kMaxRects = 16;
+constexpr int kMaxRects = 32;
 constexpr int kMaxCopies = 64;
 
 // One output rectangle of a launch, in block-local node coordinates.

@@ -34,7 +34,7 @@ bool resolve_owner(int64_t tiles_x, int64_t tiles_y, int32_t nranks,
 }
 
 Plan make_plan(int64_t nx, int64_t ny, int64_t eps, int64_t tiles_x,
-               int64_t tiles_y, const std::vector<int32_t> &owner) {
+               int64_t tiles_y, const std::vector<int32_t> &owner, bool merge) {
   Plan plan;
   const int64_t tw = nx / tiles_x, th = ny / tiles_y;
   int32_t nranks = 0;
@@ -48,8 +48,8 @@ Plan make_plan(int64_t nx, int64_t ny, int64_t eps, int64_t tiles_x,
       std::vector<TR> runs;
       for (int64_t gx = 0; gx < tiles_x;) {
         if (owner[(size_t)(gx + gy * tiles_x)] != rank) { ++gx; continue; }
-        int64_t e = gx;
-        while (e < tiles_x && owner[(size_t)(e + gy * tiles_x)] == rank) ++e;
+        int64_t e = gx + 1;
+        while (merge && e < tiles_x && owner[(size_t)(e + gy * tiles_x)] == rank) ++e;
         runs.push_back({gx, e, gy, gy + 1});
         gx = e;
       }
@@ -58,7 +58,7 @@ Plan make_plan(int64_t nx, int64_t ny, int64_t eps, int64_t tiles_x,
         auto it = std::find_if(runs.begin(), runs.end(), [&](const TR &r) {
           return r.gx0 == o.gx0 && r.gx1 == o.gx1;
         });
-        if (it != runs.end()) {
+        if (merge && it != runs.end()) {
           TR m = o;
           m.gy1 = gy + 1;
           next_open.push_back(m);

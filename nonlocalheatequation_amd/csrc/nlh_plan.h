@@ -51,7 +51,8 @@ bool resolve_owner(int64_t tiles_x, int64_t tiles_y, int32_t nranks,
 // Merge each rank's tiles into rectangles (maximal x-runs per tile row,
 // merged downwards when a run repeats) and build the halo pieces for a
 // horizon `eps`.
+// merge == false keeps every tile as its own block.
 Plan make_plan(int64_t nx, int64_t ny, int64_t eps, int64_t tiles_x,
-               int64_t tiles_y, const std::vector<int32_t> &owner);
+               int64_t tiles_y, const std::vector<int32_t> &owner, bool merge = true);
 
 }  // namespace nlh

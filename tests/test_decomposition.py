@@ -1,0 +1,195 @@
+"""CPU: the multi-rank decomposition (block plan + halo plan of libnlh) run
+with torch.distributed/gloo, world sizes 2 and 3.
+
+Each rank owns the blocks nlh_block_plan() gives it, padded by an eps halo
+(zero outside the domain), exchanges exactly the pieces nlh_halo_plan()
+lists (gloo isend/irecv between ranks, copies within a rank), and steps its
+blocks with a numpy restatement of sum_local in the reference's per-term
+order.  After nt steps every owned node must equal the global oracle bit for
+bit.  This is the GPU path's host logic (which pieces move where, blocks,
+ownership maps incl. the reference's --file maps and eps > tile size) checked
+without a GPU; tests/test_gpu_multiblock.py runs the same plans through the
+HIP kernels.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, read_input
+
+import nonlocalheatequation_amd as N
+
+torch = pytest.importorskip("torch")
+import torch.distributed as dist  # noqa: E402
+import torch.multiprocessing as mp  # noqa: E402
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _lens(eps):
+    return [int(np.floor(np.sqrt(float(eps * eps - d * d)))) for d in range(eps + 1)]
+
+
+def block_step(P, E, w, h, c2d, dh2, dt, lens):
+    """sum_local (src/2d_nonlocal_serial.cpp:256-270) on a padded block, same
+    per-term order: sx outer, sy inner, res += ((c*(u_j-u_i))*dh^2)."""
+    u = P[E:E + h, E:E + w]
+    res = np.zeros_like(u)
+    for dx in range(-E, E + 1):
+        ln = lens[abs(dx)]
+        for dy in range(-ln, ln + 1):
+            v = P[E + dy:E + dy + h, E + dx:E + dx + w]
+            res += (c2d * (v - u)) * dh2
+    return u + res * dt
+
+
+def _worker(rank, world, port, case, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import oracle as O
+        nx, ny, eps, nt, tiles, owner, split = (case[k] for k in
+                                                ("nx", "ny", "eps", "nt", "tiles", "owner", "split"))
+        k, dh = 1.0, 1.0 / nx
+        dt = eps ** 4 * dh * dh / (8 * k * N.disk_count(eps))
+        p = O.params(nx, ny, eps, k, dt, dh, 0)
+        u0 = O.test_init(p)
+        ref = O.run(p, nt, u0)
+        c2d = (k * 8) / (eps * dh) ** 4
+        lens = _lens(eps)
+        blocks = N.block_plan(nx, ny, eps, tiles, owner, world, split)
+        allp = np.concatenate([N.halo_plan(nx, ny, eps, tiles, owner, r, world, split)
+                               for r in range(world)] or [np.zeros((0, 8), np.int64)])
+        E = eps
+        mine = {bi: b for bi, b in enumerate(blocks) if b[0] == rank}
+        pad = {}
+        for bi, b in mine.items():
+            _, _, x0, y0, w, h = b
+            P = np.zeros((h + 2 * E, w + 2 * E))
+            P[E:E + h, E:E + w] = u0[y0:y0 + h, x0:x0 + w]
+            pad[bi] = P
+
+        def view(bi, gx0, gy0, w, h):
+            _, _, x0, y0, _, _ = blocks[bi]
+            return pad[bi][E + gy0 - y0:E + gy0 - y0 + h, E + gx0 - x0:E + gx0 - x0 + w]
+
+        for _ in range(nt):
+            reqs, recv = [], []
+            for pc in allp:
+                src, dst, gx0, gy0, w, h, sb, db = (int(v) for v in pc)
+                if src == rank and dst != rank:
+                    t = torch.from_numpy(np.ascontiguousarray(view(sb, gx0, gy0, w, h)))
+                    reqs.append(dist.isend(t, dst))
+                elif dst == rank and src != rank:
+                    t = torch.empty((h, w), dtype=torch.float64)
+                    reqs.append(dist.irecv(t, src))
+                    recv.append((db, gx0, gy0, w, h, t))
+                elif src == rank and dst == rank:
+                    view(db, gx0, gy0, w, h)[...] = view(sb, gx0, gy0, w, h)
+            for r in reqs:
+                r.wait()
+            for db, gx0, gy0, w, h, t in recv:
+                view(db, gx0, gy0, w, h)[...] = t.numpy()
+            new = {}
+            for bi, b in mine.items():
+                new[bi] = block_step(pad[bi], E, int(b[4]), int(b[5]), c2d, dh * dh, dt, lens)
+            for bi, b in mine.items():
+                pad[bi][E:E + int(b[5]), E:E + int(b[4])] = new[bi]
+        ok, nblk = True, 0
+        for bi, b in mine.items():
+            _, _, x0, y0, w, h = (int(v) for v in b)
+            ok &= bool(np.array_equal(pad[bi][E:E + h, E:E + w], ref[y0:y0 + h, x0:x0 + w]))
+            nblk += 1
+        q.put((rank, ok, nblk))
+    finally:
+        dist.destroy_process_group()
+
+
+CASES = [
+    dict(name="2x2 tiles locidx", nx=40, ny=60, eps=5, nt=4, tiles=(2, 2), owner=None, split=False, world=2),
+    dict(name="4s_2n file map (L-shaped owner)", nx=40, ny=40, eps=3, nt=3, tiles=(2, 2),
+         owner=[0, 1, 1, 1], split=False, world=2),
+    dict(name="eps > tile, split tiles", nx=30, ny=20, eps=7, nt=2, tiles=(6, 4), owner=None, split=True, world=3),
+    dict(name="25s_8n map folded to 3 ranks", nx=50, ny=50, eps=4, nt=3, tiles=(5, 5), owner="25s_8n",
+         split=False, world=3),
+]
+
+
+def _owner_from_file(name, world):
+    tok = read_input(f"load_balance_{name}.txt").split()
+    npx, npy = int(tok[2]), int(tok[3])
+    own = [0] * (npx * npy)
+    vals = list(map(int, tok[5:]))
+    for i in range(npx * npy):
+        px, py, loc = vals[3 * i:3 * i + 3]
+        own[px + py * npx] = loc % world
+    return own
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
+def test_gloo_decomposition_bitwise(case):
+    case = dict(case)
+    if isinstance(case["owner"], str):
+        case["owner"] = _owner_from_file(case["owner"], case["world"])
+    world = case["world"]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, case, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for pr in procs:
+        pr.join(timeout=60)
+    assert all(ok for _, ok, _ in res), res
+    assert sum(n for _, _, n in res) == len(N.block_plan(case["nx"], case["ny"], case["eps"], case["tiles"],
+                                                          case["owner"], world, case["split"]))
+
+
+def test_block_plan_covers_lattice():
+    for tiles, owner, world, split in [((5, 5), None, 8, False), ((4, 3), None, 5, True),
+                                       ((2, 2), [0, 1, 1, 1], 2, False)]:
+        b = N.block_plan(100, 60, 5, tiles, owner, world, split)
+        cover = np.zeros((60, 100), np.int32)
+        for r, _, x0, y0, w, h in b:
+            cover[y0:y0 + h, x0:x0 + w] += 1
+        assert (cover == 1).all()
+
+
+def test_halo_plan_covers_halo_exactly():
+    nx, ny, eps, tiles, world = 60, 48, 7, (6, 4), 3
+    b = N.block_plan(nx, ny, eps, tiles, None, world, True)
+    for rank in range(world):
+        pcs = N.halo_plan(nx, ny, eps, tiles, None, rank, world, True)
+        for bi, blk in enumerate(b):
+            if blk[0] != rank:
+                continue
+            _, _, x0, y0, w, h = blk
+            need = np.zeros((ny, nx), np.int32)
+            need[max(0, y0 - eps):min(ny, y0 + h + eps), max(0, x0 - eps):min(nx, x0 + w + eps)] = 1
+            need[y0:y0 + h, x0:x0 + w] = 0
+            got = np.zeros_like(need)
+            for src, dst, gx0, gy0, pw, ph, sb, db in pcs:
+                if db == bi:
+                    got[gy0:gy0 + ph, gx0:gx0 + pw] += 1
+                    sx0, sy0, sw, sh = b[sb][2:]
+                    assert sx0 <= gx0 and gx0 + pw <= sx0 + sw and sy0 <= gy0 and gy0 + ph <= sy0 + sh
+                    assert b[sb][0] == src and dst == rank
+            assert np.array_equal(got, need)
+
+
+def test_default_owner_is_locidx():
+    # locidx(): (i * nl) / (npx * npy)   src/2d_nonlocal_distributed.cpp:105-110
+    o = N.resolve_owner(5, 5, 8)
+    assert list(o) == [(i * 8) // 25 for i in range(25)]
+    with pytest.raises(N.NLHError):
+        N.resolve_owner(2, 2, 2, [0, 1, 2, 0])

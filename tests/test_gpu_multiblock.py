@@ -1,0 +1,126 @@
+"""GPU: the multi-block step (halo pieces, interior/boundary-band split,
+overlapped exchange stream) through the C ABI, on one MI355X.
+
+split_tiles=True keeps every tile as its own device block, so one rank runs
+the same halo machinery a multi-GPU run uses (local block-to-block copies in
+place of RCCL send/recv).  Exact kernel: bitwise vs the oracle; fast kernel:
+1e-12 of field scale.  The last test runs two RCCL ranks as two processes;
+RCCL refuses two ranks on one device, in which case it is skipped (the
+RCCL path then runs in the driver's multi-GPU bench; its plan is covered on
+CPU by tests/test_decomposition.py).
+"""
+import multiprocessing as mp
+import os
+
+import numpy as np
+import pytest
+
+import nonlocalheatequation_amd as N
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(nx, ny, eps, nt, test, kernel, tiles, split, owner=None, k=1.0, dt=None, dh=None, u0=None):
+    dh = dh or 1.0 / nx
+    dt = dt or eps ** 4 * dh * dh / (8 * k * N.disk_count(eps))
+    with N.Solver(nx, ny, eps, k, dt, dh, test=test, kernel=kernel, tiles=tiles,
+                  split_tiles=split, owner=owner) as s:
+        if u0 is None:
+            s.test_init()
+        else:
+            s.input_init(u0)
+        s.run(nt)
+        s.synchronize()
+        return s.field(), s.errors(nt), s.info(), (k, dt, dh)
+
+
+CASES = [
+    (64, 48, 5, 6, (2, 2)),
+    (30, 20, 7, 3, (6, 4)),      # eps > tile size: pieces from non-adjacent tiles
+    (512, 384, 8, 4, (4, 3)),    # 128x128 tiles: full strips + bands in the fast kernel
+    (300, 200, 3, 5, (3, 2)),
+]
+
+
+@pytest.mark.parametrize("nx,ny,eps,nt,tiles", CASES)
+def test_split_tiles_exact_bitwise(oracle, nx, ny, eps, nt, tiles):
+    u, (l2, li), info, (k, dt, dh) = _run(nx, ny, eps, nt, True, "exact", tiles, True)
+    assert info.nblocks == tiles[0] * tiles[1]
+    p = oracle.params(nx, ny, eps, k, dt, dh, 1)
+    ref = oracle.run(p, nt)
+    assert np.array_equal(u, ref)
+    assert li == oracle.errors(p, nt, ref)[1]
+
+
+@pytest.mark.parametrize("nx,ny,eps,nt,tiles", CASES)
+def test_split_tiles_fast(oracle, nx, ny, eps, nt, tiles):
+    rng = np.random.default_rng(7)
+    u0 = rng.uniform(-1, 1, size=(ny, nx))
+    u, _, info, (k, dt, dh) = _run(nx, ny, eps, nt, False, "fast", tiles, True, u0=u0)
+    assert info.kernel == N.KERNEL_FAST
+    p = oracle.params(nx, ny, eps, k, dt, dh, 0)
+    ref = oracle.run(p, nt, u0)
+    assert np.max(np.abs(u - ref)) <= 1e-12 * np.max(np.abs(ref))
+
+
+def test_merged_vs_split_identical():
+    a = _run(256, 256, 6, 5, False, "fast", (4, 4), False)[0]
+    b = _run(256, 256, 6, 5, False, "fast", (4, 4), True)[0]
+    # same arithmetic per node whatever the blocking
+    assert np.array_equal(a, b)
+
+
+def test_single_rank_owner_map_from_file(oracle):
+    # tests/load_balance_4s_2n.txt: 20x20 tiles, 2x2, dh=0.0025; all tiles on one GPU
+    nx = ny = 40
+    u, (l2, li), info, _ = _run(nx, ny, 5, 10, True, "exact", (2, 2), False, owner=[0, 0, 0, 0],
+                                k=1.0, dt=0.0005, dh=0.0025)
+    p = oracle.params(nx, ny, 5, 1.0, 0.0005, 0.0025, 1)
+    assert np.array_equal(u, oracle.run(p, 10))
+
+
+def _rccl_rank(rank, cid, q):
+    try:
+        nx = ny = 256
+        eps = 8
+        dh = 1.0 / nx
+        dt = eps ** 4 * dh * dh / (8 * N.disk_count(eps))
+        with N.Solver(nx, ny, eps, 1.0, dt, dh, test=False, kernel="fast", device=0, rank=rank,
+                      nranks=2, tiles=(2, 1), comm_id=cid) as s:
+            s.test_init()
+            s.run(5)
+            s.synchronize()
+            u = s.gather(0)
+            q.put((rank, "ok", u if rank == 0 else None))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, "err", str(e)))
+
+
+def test_rccl_two_ranks_one_gpu(oracle):
+    cid = N.comm_unique_id()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_rccl_rank, args=(r, cid, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = {}
+    try:
+        for _ in range(2):
+            r, st, v = q.get(timeout=180)
+            res[r] = (st, v)
+    finally:
+        for p in ps:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    errs = [v for st, v in res.values() if st == "err"]
+    if errs:
+        if any("uplicate" in e or "invalid usage" in e.lower() for e in errs):
+            pytest.skip(f"RCCL refuses two ranks on one GPU: {errs[0][:160]}")
+        pytest.fail(str(errs))
+    nx = 256
+    dh = 1.0 / nx
+    dt = 8 ** 4 * dh * dh / (8 * N.disk_count(8))
+    ref = oracle.run(oracle.params(nx, nx, 8, 1.0, dt, dh, 0), 5)
+    u = res[0][1]
+    assert np.max(np.abs(u - ref)) <= 1e-12 * np.max(np.abs(ref))

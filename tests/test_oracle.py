@@ -1,0 +1,128 @@
+"""CPU: pin the oracle (oracle/nlh_oracle.c) against the reference's outputs.
+
+known_answers.json holds the reference serial solver's own outputs (SURVEY.md
+Appendix A).  The oracle must reproduce them bit for bit; the tiled restatement
+of 2d_nonlocal_async must equal the serial one bit for bit; and the reference's
+batch contract (error_l2 / N <= 1e-6, CMakeLists.txt:101-154) must hold on all
+three batch files.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, read_input
+
+import nonlocalheatequation_amd as N
+
+KA = json.load(open(os.path.join(ROOT, "tests", "golden", "known_answers.json")))
+GOLD = os.path.join(ROOT, "tests", "golden")
+
+
+def _seq_sum(u):
+    s = 0.0
+    for v in u.ravel():  # storage order, sequential (as the survey summed)
+        s += float(v)
+    return s
+
+
+@pytest.mark.parametrize("i", range(len(KA["serial_2d_txt"])))
+def test_oracle_matches_reference_serial(oracle, i):
+    a = KA["serial_2d_txt"][i]
+    p = oracle.params(a["nx"], a["ny"], a["eps"], a["k"], a["dt"], a["dh"], 1)
+    u = oracle.run(p, a["nt"])
+    l2, li = oracle.errors(p, a["nt"], u)
+    assert l2 == a["l2"]
+    assert li == a["linf"]
+    assert float(u[1, 1]) == a["u_1_1"]
+    if a["nx"] * a["ny"] <= 2500:
+        assert _seq_sum(u) == a["sum_u"]
+
+
+@pytest.mark.parametrize("i", range(len(KA["tiled_rows_global"])))
+def test_oracle_matches_reference_tiled_rows(oracle, i):
+    a = KA["tiled_rows_global"][i]
+    p = oracle.params(a["nx"], a["ny"], a["eps"], a["k"], a["dt"], a["dh"], 1)
+    u = oracle.run(p, a["nt"])
+    l2, li = oracle.errors(p, a["nt"], u)
+    assert l2 == a["l2"]
+    assert li == a["linf"]
+
+
+@pytest.mark.parametrize("fmt,name", [("serial", "2d.txt"), ("async", "2d_async.txt"),
+                                      ("distributed", "2d_distributed.txt")])
+def test_reference_batch_contract(oracle, fmt, name):
+    for r in N.parse_batch(read_input(name), fmt):
+        p = oracle.params(r.nx, r.ny, r.eps, r.k, r.dt, r.dh, 1)
+        u = oracle.run(p, r.nt)
+        l2, _ = oracle.errors(p, r.nt, u)
+        assert l2 / (r.nx * r.ny) <= 1e-6
+
+
+def test_tiled_equals_serial(oracle):
+    # 2d_nonlocal_async execution model (tile tasks + barrier) == serial, bitwise
+    for tiles in [(1, 1), (2, 2), (5, 3), (20, 20)]:
+        p = oracle.params(40, 60, 5, 0.2, 0.001, 0.02, 1)
+        ref = oracle.run(p, 7)
+        u = oracle.test_init(p)
+        oracle.run_tiled(p, 7, tiles[0], tiles[1], u, 4)
+        assert np.array_equal(u, ref), tiles
+
+
+def test_thread_count_invariance(oracle):
+    p = oracle.params(37, 29, 4, 1.0, 0.0005, 0.02, 1)
+    a = oracle.run(p, 5, nthreads=1)
+    b = oracle.run(p, 5, nthreads=7)
+    assert np.array_equal(a, b)
+
+
+def test_disk_counts(oracle):
+    # SURVEY.md 3.4 note 1
+    for eps, n in [(3, 29), (5, 81), (6, 113), (8, 197), (10, 317), (16, 797), (32, 3209)]:
+        assert oracle.disk_count(eps) == n
+        assert N.disk_count(eps) == n
+
+
+def test_golden_fields_reproduce(oracle):
+    rows = {0: (50, 50, 45, 5, 1.0, 0.0005, 0.02), 5: (40, 40, 200, 3, 0.2, 0.001, 0.02),
+            7: (40, 40, 200, 8, 0.2, 0.001, 0.02)}
+    for r, (nx, ny, nt, eps, k, dt, dh) in rows.items():
+        for test in (0, 1):
+            g = np.load(os.path.join(GOLD, f"fields_2d_row{r}_test{test}.npy"))
+            p = oracle.params(nx, ny, eps, k, dt, dh, test)
+            assert np.array_equal(oracle.run(p, nt), g)
+
+
+def test_per_step_l2_fixture(oracle):
+    g = np.load(os.path.join(GOLD, "l2_per_step_row0.npy"))
+    p = oracle.params(50, 50, 5, 1.0, 0.0005, 0.02, 1)
+    u = oracle.test_init(p)
+    for t in range(45):
+        u = oracle.step(p, t, u)
+        assert oracle.errors(p, t + 1, u)[0] == g[t]
+    assert g[-1] == KA["serial_2d_txt"][0]["l2"]
+
+
+def test_long_run_known_answer(oracle):
+    a = KA["long_runs_eps8"][0]  # 64^2, eps=8, 1000 steps
+    dh = 1.0 / a["nx"]
+    dt = 8 ** 4 * dh * dh / (8 * 1.0 * oracle.disk_count(8))
+    p = oracle.params(a["nx"], a["ny"], 8, 1.0, dt, dh, 1)
+    u = oracle.run(p, a["nt"])
+    l2, _ = oracle.errors(p, a["nt"], u)
+    assert l2 == a["l2"]
+
+
+def test_stdin_ic_order(oracle):
+    # input_init reads sx outer (src/2d_nonlocal_serial.cpp:180-187): a stream
+    # v0 v1 ... lands at index sx + sy*nx in sx-major order
+    nx, ny = 3, 2
+    stream = np.arange(nx * ny, dtype=np.float64)
+    u = np.empty(nx * ny)
+    i = 0
+    for sx in range(nx):
+        for sy in range(ny):
+            u[sx + sy * nx] = stream[i]
+            i += 1
+    assert list(u) == [0, 2, 4, 1, 3, 5]
