@@ -20,6 +20,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -83,6 +84,7 @@ struct nlh_solver {
   std::vector<LocalBlock> blocks;
   int device = 0;
   int kernel = NLH_KERNEL_EXACT;
+  int fast_r = 2;  // columns per lane of the fast kernel (NLH_FAST_R=4: 256-column strips)
   hipStream_t s_main = nullptr, s_comm = nullptr;
   hipEvent_t ev_ready = nullptr, ev_halo = nullptr;
   int64_t t = 0;
@@ -159,7 +161,7 @@ std::vector<LRect> split_block(const LocalBlock &b, int E, int sw) {
 int build_rectlists(nlh_solver *s) {
   const int E = (int)s->p.eps;
   const bool fast = s->kernel == NLH_KERNEL_FAST;
-  const int sw = fast ? nlh::fast_strip_width(E) : 64;
+  const int sw = fast ? nlh::fast_strip_width(E, s->fast_r) : 64;
   // gather local rects
   struct Item { int blk; LRect r; };
   std::vector<Item> all, inter, bnd;
@@ -170,13 +172,14 @@ int build_rectlists(nlh_solver *s) {
       (r.interior ? inter : bnd).push_back(it);
     }
   }
-  // segment height for the fast kernel: aim at ~2048 single-wave workgroups
+  // segment height for the fast kernel: ~1024 single-wave workgroups (4 per CU,
+  // all resident at once; balanced grids measured fastest, profiles/r01/tune_*.json)
   int seg_h = 4;
   if (fast) {
     int64_t strip_rows = 0;
     for (auto &it : all) strip_rows += ceil_div(it.r.x1 - it.r.x0, sw) * (it.r.y1 - it.r.y0);
     seg_h = s->p.seg_rows > 0 ? s->p.seg_rows
-                              : (int)std::max<int64_t>(nlh::fast_seg_min(E), ceil_div(strip_rows, 2048));
+                              : (int)std::max<int64_t>(nlh::fast_seg_min(E), ceil_div(strip_rows, 1024));
   }
   s->sc.seg_h = seg_h;
   auto make = [&](const std::vector<Item> &items, int k, std::vector<nlh::RectList> &out) -> int {
@@ -308,7 +311,7 @@ int launch_stencil(nlh_solver *s, const std::vector<nlh::RectList> &v) {
     if (rl.nwork == 0) continue;
     int rc;
     if (s->kernel == NLH_KERNEL_FAST)
-      rc = nlh::launch_fast(rl, s->sc, test, s->s_main);
+      rc = nlh::launch_fast(rl, s->sc, test, s->fast_r, s->s_main);
     else
       rc = nlh::launch_exact(rl, s->sc, test, s->s_main);
     if (rc != 0) return fail(NLH_ERR_HIP, std::string("stencil launch failed: ") + hipGetErrorString((hipError_t)rc));
@@ -474,6 +477,8 @@ int create_impl(const nlh_params *pin, nlh_solver *s) {
     kern = NLH_KERNEL_EXACT;
   }
   s->kernel = kern;
+  if (const char *r = std::getenv("NLH_FAST_R")) s->fast_r = std::atoi(r) == 4 ? 4 : 2;
+  s->fast_r = nlh::fast_lanes_cols(E, s->fast_r);
 
   HIP_TRY(hipStreamCreateWithFlags(&s->s_main, hipStreamNonBlocking));
   HIP_TRY(hipStreamCreateWithFlags(&s->s_comm, hipStreamNonBlocking));
@@ -516,7 +521,7 @@ int create_impl(const nlh_params *pin, nlh_solver *s) {
     b.plan_index = (int)i;
     b.r = bd.r;
     b.xl = (int32_t)XL;
-    b.pitch = XL + round_up(b.r.w, 128) + XL;
+    b.pitch = XL + round_up(b.r.w, 256) + XL;  // whole 256-column strips stay in bounds
     b.rows = b.r.h + 2 * E;
     b.L = b.r.x0 > 0;
     b.Rr = b.r.x0 + b.r.w < p.nx;

@@ -79,10 +79,11 @@ struct NormPartial {
 // ---- launch API (nlh_kernels.hip) -----------------------------------------
 // Returns false if (E, R) has no fast instantiation.
 bool fast_supported(int E);
-int fast_strip_width(int E);    // 64*R columns per strip
-int fast_seg_min(int E);        // smallest sensible segment height
+int fast_lanes_cols(int E, int want_r);   // R actually used (2 or 4)
+int fast_strip_width(int E, int want_r);  // 64*R columns per strip
+int fast_seg_min(int E);                  // smallest sensible segment height
 // Work-item counts are filled into rl by the caller (wg_begin/nwork).
-int launch_fast(const RectList &rl, const StepConst &c, bool test, void *stream);
+int launch_fast(const RectList &rl, const StepConst &c, bool test, int want_r, void *stream);
 int launch_exact(const RectList &rl, const StepConst &c, bool test, void *stream);
 // A = sum_local(u) only (no time update) -- used once for L_h[W0].
 int launch_exact_sum(const RectList &rl, const StepConst &c, void *stream);

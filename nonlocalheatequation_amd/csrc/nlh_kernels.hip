@@ -59,6 +59,12 @@ __host__ __device__ constexpr int clen(int E, int d) {
   return L;
 }
 
+__host__ __device__ constexpr int pow2_ceil(int v) {
+  int p = 1;
+  while (p < v) p <<= 1;
+  return p;
+}
+
 __host__ __device__ constexpr int disk_count(int E) {
   int n = 0;
   for (int d = -E; d <= E; ++d) n += 2 * clen(E, d < 0 ? -d : d) + 1;
@@ -154,37 +160,53 @@ __global__ __launch_bounds__(256) void k_exact(RectList L, StepConst C) {
 // ----------------------------------------------------------------------------
 // k_fast: nested-window strip sweep.  See the file header.
 //   E  horizon, R columns per lane (strip = 64*R columns), D rows in flight.
+//
+// Per wave: one strip of W = 64*R output columns over one segment of rows.
+// Input rows stream through an LDS ring of K = next_pow2(E+D+1) slots
+// (LDS-DMA issued D rows ahead); a row stays in the ring E rows after its
+// window was consumed, so the centre value u(x, y) of the update is read back
+// from it (slot arithmetic is a mask, no register shifting).  Odd segments sweep upwards
+// so that the 2E rows two neighbouring segments both read are fetched at the
+// same time (L2 hits instead of a second trip to HBM); work items run
+// strip-fastest so horizontally adjacent strips, which share EP halo
+// columns, are co-resident on one XCD.
 template <int E, int R, int D, bool TEST>
 __global__ __launch_bounds__(64) void k_fast(RectList L, StepConst C) {
-  constexpr int P = 2 * E + 1;          // ring slots == accumulator period
+  constexpr int P = 2 * E + 1;          // accumulator period (static unroll)
   constexpr int W = 64 * R;             // strip width (outputs)
   constexpr int EP = (E + 1) & ~1;      // halo columns staged per side
   constexpr int RW = W + 2 * EP;        // doubles per ring row
   constexpr int NCH = RW / 2;           // 16-byte chunks per row
+  constexpr int K = pow2_ceil(E + D + 1);  // ring slots (power of two)
   constexpr int GU = (NCH + 63) / 64;   // DMA instructions per u row
   constexpr int GL = TEST ? (W / 2 + 63) / 64 : 0;  // per L_h[W0] row
   constexpr int G = GU + GL;
   constexpr int OFF = EP - E;           // window start inside a staged row
-  static_assert(D >= 1 && D <= E, "ring slot reuse needs D <= E");
+  static_assert(D >= 1, "prefetch distance");
   static_assert(D * G < 64, "vmcnt range");
 
-  __shared__ __attribute__((aligned(16))) double ring[P * RW + (TEST ? P * W : 0)];
-  double *lwr = ring + P * RW;  // L_h[W0] ring (TEST)
+  __shared__ __attribute__((aligned(16))) double ring[K * RW + (TEST ? K * W : 0)];
+  double *lwr = ring + K * RW;  // L_h[W0] ring (TEST)
 
   const int lane = (int)threadIdx.x;
   const int work = xcd_remap(blockIdx.x, gridDim.x);
   const int ri = find_rect(L, work);
   const Rect &Rc = L.r[ri];
   const int local = work - Rc.wg_begin;
-  const int strip = local / Rc.nseg, seg = local % Rc.nseg;
+  const int strip = local % Rc.nstrip, seg = local / Rc.nstrip;
   const int x0 = Rc.x0 + strip * W;
   const int Y0 = Rc.y0 + seg * C.seg_h;
   const int Y1 = min(Y0 + C.seg_h, Rc.y1);
   const int n_in = (Y1 - Y0) + 2 * E;   // input rows Y0-E .. Y1+E-1
+  const bool up = (seg & 1) != 0;       // sweep direction
   const int64_t pitch = Rc.pitch;
+  const int64_t stride = up ? -pitch : pitch;
+  const int yfirst = up ? (Y1 + E - 1) : (Y0 - E);  // block-local row of input 0
 
-  const double *g0 = Rc.u + (int64_t)(Y0 - E) * pitch + (x0 - EP);
-  const double *l0 = TEST ? Rc.lw + (int64_t)(Y0 - E) * pitch + x0 : nullptr;
+  const double *g0 = Rc.u + (int64_t)yfirst * pitch + (x0 - EP);
+  // L_h[W0] row of the output emitted at iteration j (j >= 2E): Y0 + j - 2E
+  // sweeping down, Y1 - 1 - (j - 2E) sweeping up
+  const double *l0 = TEST ? Rc.lw + (int64_t)(up ? Y1 - 1 : Y0) * pitch + x0 : nullptr;
   const uint32_t lring = __builtin_amdgcn_readfirstlane(lds_addr(ring));
   const uint32_t llw = __builtin_amdgcn_readfirstlane(lds_addr(lwr));
 
@@ -199,32 +221,37 @@ __global__ __launch_bounds__(64) void k_fast(RectList L, StepConst C) {
     }
   }
 
-  auto issue_row = [&](int row, int slot) {
-    const int rr = min(row, n_in - 1);
-    dma_chunks<NCH>(g0 + (int64_t)rr * pitch, lring + slot * RW * 8, lane);
-    if (TEST) dma_chunks<W / 2>(l0 + (int64_t)rr * pitch, llw + slot * W * 8, lane);
+  // rows i of the u stream, and L_h rows for the output of iteration i
+  auto issue = [&](int i, int slot) {
+    const int rr = min(i, n_in - 1);
+    dma_chunks<NCH>(g0 + (int64_t)rr * stride, lring + slot * RW * 8, lane);
+    if (TEST) {
+      const int lr = min(max(i - 2 * E, 0), n_in - 2 * E - 1);
+      dma_chunks<W / 2>(l0 + (int64_t)lr * stride, llw + slot * W * 8, lane);
+    }
   };
 
 #pragma unroll
-  for (int s = 0; s < D; ++s) issue_row(s, s);
+  for (int s = 0; s < D; ++s) issue(s, s);
 
   double acc[R][P];
 #pragma unroll
   for (int c = 0; c < R; ++c)
 #pragma unroll
     for (int j = 0; j < P; ++j) acc[c][j] = 0.0;
-
+  int bs = 0;  // b % K
   for (int b = 0; b < n_in; b += P) {
 #pragma unroll
     for (int q = 0; q < P; ++q) {
       const int i = b + q;
       if (i < n_in) {
-        issue_row(i + D, (q + D) % P);
+        const int slot = (bs + q) & (K - 1);
+        issue(i + D, (bs + q + D) & (K - 1));
         wait_vmcnt<D * G>();
 
         // window of this lane: columns xl-E .. xl+R-1+E
         double w[R + 2 * E];
-        const double *rowp = ring + q * RW;
+        const double *rowp = ring + slot * RW;
         if constexpr (R == 2) {
           constexpr int NB = (OFF + 2 * E + 2 + 1) / 2;
           const double2 *rp = reinterpret_cast<const double2 *>(rowp + 2 * lane);
@@ -256,14 +283,12 @@ __global__ __launch_bounds__(64) void k_fast(RectList L, StepConst C) {
           }
         }
 
-        // output row i-E is complete: slot (q - E) mod P
-        constexpr int dummy = 0;
-        (void)dummy;
+        // output of input row i-E is complete: accumulator (q - E) mod P
         const int so = (q + E + 1) % P;
         if (i >= 2 * E) {
-          const int y = Y0 + i - 2 * E;
-          const double *crow = ring + so * RW + EP + R * lane;
+          const int y = up ? (Y1 - 1 - (i - 2 * E)) : (Y0 + i - 2 * E);
           double out[R];
+          const double *crow = ring + ((bs + q - E) & (K - 1)) * RW + EP + R * lane;
 #pragma unroll
           for (int c = 0; c < R; ++c) {
             const double uc = crow[c];
@@ -272,7 +297,7 @@ __global__ __launch_bounds__(64) void k_fast(RectList L, StepConst C) {
           }
           if (TEST) {
             const double syv = C.syt[Rc.gy0 + y + E];
-            const double *lrow = lwr + so * W + R * lane;
+            const double *lrow = lwr + slot * W + R * lane;
 #pragma unroll
             for (int c = 0; c < R; ++c) {
               const double w0 = sxv[c] * syv;
@@ -295,6 +320,7 @@ __global__ __launch_bounds__(64) void k_fast(RectList L, StepConst C) {
         for (int c = 0; c < R; ++c) acc[c][so] = 0.0;
       }
     }
+    bs = (bs + P) & (K - 1);
   }
   wait_vmcnt<0>();  // drain the clamped tail DMAs before the wave retires
 }
@@ -378,42 +404,47 @@ static int check_launch() {
   return e == hipSuccess ? 0 : (int)e;
 }
 
-// compile-time dispatch table for the fast kernel
-template <int E>
-struct FastCfg {
-  static constexpr int R = 2;
-  static constexpr int D = (E < 6) ? E : 6;
-};
+// compile-time dispatch table for the fast kernel: R = 2 (128-column strips)
+// for every E <= 12, R = 4 (256-column strips) for E <= 8.
+constexpr int kFastMaxE = 12;   // E >= 13 spills the accumulator file
+constexpr int kFastMaxE4 = 8;   // widest E with a 256-column variant
+constexpr int kFastD = 6;       // rows in flight per wave
 
-template <int E, bool TEST>
-static int launch_fast_e(const RectList &rl, const StepConst &c, hipStream_t st) {
-  constexpr int R = FastCfg<E>::R, D = FastCfg<E>::D;
-  hipLaunchKernelGGL((k_fast<E, R, D, TEST>), dim3(rl.nwork), dim3(64), 0, st, rl, c);
+template <int E, int R, bool TEST>
+static int launch_fast_er(const RectList &rl, const StepConst &c, hipStream_t st) {
+  hipLaunchKernelGGL((k_fast<E, R, kFastD, TEST>), dim3(rl.nwork), dim3(64), 0, st, rl, c);
   return check_launch();
 }
 
 template <int E>
-static int launch_fast_dispatch(int e, const RectList &rl, const StepConst &c,
-                                bool test, hipStream_t st) {
+static int launch_fast_dispatch(int e, int r, const RectList &rl, const StepConst &c, bool test,
+                                hipStream_t st) {
   if constexpr (E == 0) {
     return -1;
   } else {
-    if (e == E) return test ? launch_fast_e<E, true>(rl, c, st) : launch_fast_e<E, false>(rl, c, st);
-    return launch_fast_dispatch<E - 1>(e, rl, c, test, st);
+    if (e == E) {
+      if constexpr (E <= kFastMaxE4) {
+        if (r == 4)
+          return test ? launch_fast_er<E, 4, true>(rl, c, st) : launch_fast_er<E, 4, false>(rl, c, st);
+      }
+      return test ? launch_fast_er<E, 2, true>(rl, c, st) : launch_fast_er<E, 2, false>(rl, c, st);
+    }
+    return launch_fast_dispatch<E - 1>(e, r, rl, c, test, st);
   }
 }
 
-constexpr int kFastMaxE = 12;  // E >= 13 spills the accumulator file (next round: two-ring design)
-
 bool fast_supported(int E) { return E >= 1 && (E <= kFastMaxE); }
 
-int fast_strip_width(int E) { return 128; }
+int fast_lanes_cols(int E, int want_r) { return (want_r == 4 && E <= kFastMaxE4) ? 4 : 2; }
+
+int fast_strip_width(int E, int r) { return 64 * fast_lanes_cols(E, r); }
 
 int fast_seg_min(int E) { return 2 * E; }
 
-int launch_fast(const RectList &rl, const StepConst &c, bool test, void *stream) {
+int launch_fast(const RectList &rl, const StepConst &c, bool test, int r, void *stream) {
   if (!fast_supported(c.E)) return -1;
-  return launch_fast_dispatch<kFastMaxE>(c.E, rl, c, test, (hipStream_t)stream);
+  return launch_fast_dispatch<kFastMaxE>(c.E, fast_lanes_cols(c.E, r), rl, c, test,
+                                         (hipStream_t)stream);
 }
 
 int launch_exact(const RectList &rl, const StepConst &c, bool test, void *stream) {

@@ -63,11 +63,15 @@ def test_split_tiles_fast(oracle, nx, ny, eps, nt, tiles):
     assert np.max(np.abs(u - ref)) <= 1e-12 * np.max(np.abs(ref))
 
 
-def test_merged_vs_split_identical():
+def test_merged_vs_split_consistent():
     a = _run(256, 256, 6, 5, False, "fast", (4, 4), False)[0]
     b = _run(256, 256, 6, 5, False, "fast", (4, 4), True)[0]
-    # same arithmetic per node whatever the blocking
-    assert np.array_equal(a, b)
+    # the fast kernel's row order (sweep direction alternates per segment)
+    # follows the blocking, so results agree to summation rounding only
+    assert np.max(np.abs(a - b)) <= 1e-13 * np.max(np.abs(a))
+    ea = _run(256, 256, 6, 5, False, "exact", (4, 4), False)[0]
+    eb = _run(256, 256, 6, 5, False, "exact", (4, 4), True)[0]
+    assert np.array_equal(ea, eb)  # the parity kernel is blocking-independent
 
 
 def test_single_rank_owner_map_from_file(oracle):

@@ -1,0 +1,124 @@
+// bw_probe.hip -- calibration of achievable HBM bandwidth for the stencil's
+// access pattern on MI355X (tools only; not part of libnlh).
+//
+//   copy_vec   : un = u over the padded 4096^2 interior, 16 B per lane,
+//                grid-stride (the guide's "float4 copy" ceiling)
+//   strip_dma  : the fast kernel's memory structure with no arithmetic:
+//                one wave per (strip, segment), rows streamed HBM -> LDS ring by
+//                global_load_lds_dwordx4 D rows ahead, each row's 128 centre
+//                values stored back from LDS
+// Prints one JSON line per variant: time per launch and GB/s (16 B / node).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                             \
+  do {                                                                    \
+    hipError_t e = (x);                                                   \
+    if (e != hipSuccess) {                                                \
+      std::fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e));         \
+      std::exit(1);                                                       \
+    }                                                                     \
+  } while (0)
+
+constexpr int N = 4096, E = 8, XL = 8, PITCH = XL + N + XL + 112;  // 4224
+constexpr int ROWS = N + 2 * E;
+
+__device__ __forceinline__ void dma16(const void *g, uint32_t lds) {
+  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" : : "v"(g), "s"(lds) : "memory");
+}
+template <int NN>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" : : "n"(NN) : "memory");
+}
+__device__ __forceinline__ uint32_t lds_addr(const void *p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
+}
+
+__global__ __launch_bounds__(256) void copy_vec(const double *__restrict__ u, double *__restrict__ un) {
+  const int64_t n2 = (int64_t)N * N / 2;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n2; e += (int64_t)gridDim.x * 256) {
+    const int64_t k = 2 * e;
+    const int64_t y = k / N, x = k % N;
+    const int64_t o = (y + E) * PITCH + XL + x;
+    *reinterpret_cast<double2 *>(un + o) = *reinterpret_cast<const double2 *>(u + o);
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(64) void strip_dma(const double *__restrict__ u, double *__restrict__ un,
+                                                int seg_h, int nstrip) {
+  constexpr int RW = 128 + 16, K = D + 1;
+  __shared__ __attribute__((aligned(16))) double ring[K * RW];
+  const int lane = threadIdx.x;
+  const int work = blockIdx.x;
+  const int strip = work % nstrip, seg = work / nstrip;
+  const int x0 = strip * 128, Y0 = seg * seg_h, Y1 = min(Y0 + seg_h, N);
+  const int n_in = Y1 - Y0 + 2 * E;
+  const double *g0 = u + (int64_t)(Y0) * PITCH + XL + x0 - 8;  // padded row Y0 - E + E
+  const uint32_t lr = __builtin_amdgcn_readfirstlane(lds_addr(ring));
+  auto issue = [&](int i, int slot) {
+    const int rr = min(i, n_in - 1);
+    const double *g = g0 + (int64_t)rr * PITCH;
+    dma16(g + 2 * lane, lr + slot * RW * 8);
+    if (lane < 8) dma16(g + 128 + 2 * lane, lr + slot * RW * 8 + 1024);
+  };
+  for (int s = 0; s < D; ++s) issue(s, s);
+  for (int i = 0; i < n_in; ++i) {
+    issue(i + D, (i + D) % K);
+    wait_vm<2 * D>();
+    const double2 v = *reinterpret_cast<const double2 *>(&ring[(i % K) * RW + 8 + 2 * lane]);
+    if (i >= 2 * E) {
+      const int y = Y0 + i - 2 * E;
+      *reinterpret_cast<double2 *>(un + (int64_t)(y + E) * PITCH + XL + x0 + 2 * lane) = v;
+    }
+  }
+  wait_vm<0>();
+}
+
+template <class F>
+static float time_it(F f, int reps) {
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  for (int i = 0; i < 5; ++i) f();
+  CK(hipEventRecord(a));
+  for (int i = 0; i < reps; ++i) f();
+  CK(hipEventRecord(b));
+  CK(hipEventSynchronize(b));
+  float ms;
+  CK(hipEventElapsedTime(&ms, a, b));
+  return ms / reps;
+}
+
+int main() {
+  const size_t bytes = (size_t)PITCH * ROWS * sizeof(double);
+  double *u, *un;
+  CK(hipMalloc(&u, bytes));
+  CK(hipMalloc(&un, bytes));
+  CK(hipMemset(u, 0, bytes));
+  CK(hipMemset(un, 0, bytes));
+  const double algo = 16.0 * N * N;
+  for (int g : {1024, 2048, 4096, 8192}) {
+    const float ms = time_it([&] { copy_vec<<<g, 256>>>(u, un); }, 50);
+    std::printf("{\"variant\": \"copy_vec\", \"grid\": %d, \"us\": %.2f, \"GBps\": %.1f}\n", g, ms * 1e3,
+                algo / (ms * 1e-3) / 1e9);
+  }
+  const int nstrip = N / 128;
+  for (int seg : {32, 43, 64, 128}) {
+    const int nseg = (N + seg - 1) / seg;
+    float ms4 = time_it([&] { strip_dma<4><<<nstrip * nseg, 64>>>(u, un, seg, nstrip); }, 50);
+    float ms8 = time_it([&] { strip_dma<8><<<nstrip * nseg, 64>>>(u, un, seg, nstrip); }, 50);
+    float ms12 = time_it([&] { strip_dma<12><<<nstrip * nseg, 64>>>(u, un, seg, nstrip); }, 50);
+    std::printf("{\"variant\": \"strip_dma\", \"seg\": %d, \"wgs\": %d, \"us_D4\": %.2f, \"us_D8\": %.2f, "
+                "\"us_D12\": %.2f, \"GBps_best\": %.1f}\n",
+                seg, nstrip * nseg, ms4 * 1e3, ms8 * 1e3, ms12 * 1e3,
+                algo / (std::min(ms4, std::min(ms8, ms12)) * 1e-3) / 1e9);
+  }
+  CK(hipFree(u));
+  CK(hipFree(un));
+  return 0;
+}

@@ -23,18 +23,22 @@ def main():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--test", action="store_true")
+    ap.add_argument("--rs", default="2", help="comma list of columns-per-lane variants (2,4)")
     a = ap.parse_args()
     n, eps = a.n, a.eps
     dh = 1.0 / n
     dt = eps ** 4 * dh * dh / (8 * N.disk_count(eps))
     segs = [int(s) for s in a.segs.split(",")]
     solvers = {}
-    for sg in segs:
-        s = N.Solver(n, n, eps, 1.0, dt, dh, test=a.test, kernel="fast", device=0, seg_rows=sg)
-        s.test_init()
-        s.run(10)
-        s.synchronize()
-        solvers[sg] = s
+    for r in [int(v) for v in a.rs.split(",")]:
+        os.environ["NLH_FAST_R"] = str(r)
+        for sg in segs:
+            s = N.Solver(n, n, eps, 1.0, dt, dh, test=a.test, kernel="fast", device=0, seg_rows=sg)
+            s.test_init()
+            s.run(10)
+            s.synchronize()
+            solvers[(r, sg)] = s
+    segs = list(solvers)
     res = {sg: [] for sg in segs}
     for _ in range(a.rounds):
         for sg, s in solvers.items():
@@ -47,7 +51,7 @@ def main():
     out = []
     for sg in segs:
         us = min(res[sg])
-        out.append({"seg_rows": sg, "us_min": us, "us_all": res[sg],
+        out.append({"r": sg[0], "seg_rows": sg[1], "us_min": us, "us_all": res[sg],
                     "gnode_s": n * n / us / 1e3, "gb_s": 16 * n * n / us / 1e3})
     print(json.dumps({"eps": eps, "n": n, "test": a.test, "results": out}))
 
