@@ -17,7 +17,12 @@ INC     := -Iinclude -I$(CSRC)
 HIPFLAGS := --offload-arch=$(ARCH) -O3 $(CXXSTD) -fPIC $(WARN) $(INC) -munsafe-fp-atomics
 HOSTFLAGS := -O2 $(CXXSTD) -fPIC $(WARN) $(INC) -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include
 
-LIB_OBJS := $(OBJDIR)/nlh_kernels.o $(OBJDIR)/nlh_api.o $(OBJDIR)/nlh_plan.o
+FAST_UNITS := $(sort $(wildcard $(CSRC)/nlh_fast_e*.hip))
+FAST_OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(FAST_UNITS))
+LIB_OBJS := $(OBJDIR)/nlh_kernels.o $(FAST_OBJS) $(OBJDIR)/nlh_api.o $(OBJDIR)/nlh_plan.o
+# the fast kernel is fully unrolled over 2E+1 rows; lift LLVM's pragma-unroll
+# size cap so every accumulator stays in registers (no scratch)
+UNROLL  := -mllvm -pragma-unroll-threshold=1000000
 DRIVERS  := $(BINDIR)/2d_nonlocal_serial $(BINDIR)/2d_nonlocal_async $(BINDIR)/2d_nonlocal_distributed
 DRV_COMMON := $(OBJDIR)/driver_common.o $(OBJDIR)/vtu_writer.o
 
@@ -30,8 +35,13 @@ oracle:
 $(OBJDIR) $(LIBDIR) $(BINDIR):
 	mkdir -p $@
 
-$(OBJDIR)/nlh_kernels.o: $(CSRC)/nlh_kernels.hip $(CSRC)/nlh_device.h | $(OBJDIR)
+KHDRS := $(CSRC)/nlh_device.h $(CSRC)/nlh_kernel_common.h $(CSRC)/nlh_fast.h
+
+$(OBJDIR)/nlh_kernels.o: $(CSRC)/nlh_kernels.hip $(KHDRS) | $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OBJDIR)/nlh_fast_%.o: $(CSRC)/nlh_fast_%.hip $(KHDRS) | $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) $(UNROLL) -c $< -o $@
 
 $(OBJDIR)/nlh_api.o: $(CSRC)/nlh_api.cpp $(CSRC)/nlh_device.h $(CSRC)/nlh_plan.h include/nlh.h | $(OBJDIR)
 	$(HIPCC) $(HOSTFLAGS) -x c++ -c $< -o $@

@@ -84,7 +84,7 @@ struct nlh_solver {
   std::vector<LocalBlock> blocks;
   int device = 0;
   int kernel = NLH_KERNEL_EXACT;
-  int fast_r = 2;  // columns per lane of the fast kernel (NLH_FAST_R=4: 256-column strips)
+  int fast_r = 2;  // columns per lane of the fast kernel (NLH_FAST_R=1|2|4: 64/128/256-column strips)
   hipStream_t s_main = nullptr, s_comm = nullptr;
   hipEvent_t ev_ready = nullptr, ev_halo = nullptr;
   int64_t t = 0;
@@ -477,7 +477,10 @@ int create_impl(const nlh_params *pin, nlh_solver *s) {
     kern = NLH_KERNEL_EXACT;
   }
   s->kernel = kern;
-  if (const char *r = std::getenv("NLH_FAST_R")) s->fast_r = std::atoi(r) == 4 ? 4 : 2;
+  if (const char *r = std::getenv("NLH_FAST_R")) {
+    const int v = std::atoi(r);
+    s->fast_r = (v == 1 || v == 4) ? v : 2;
+  }
   s->fast_r = nlh::fast_lanes_cols(E, s->fast_r);
 
   HIP_TRY(hipStreamCreateWithFlags(&s->s_main, hipStreamNonBlocking));

@@ -30,79 +30,11 @@
 
 #include <cstdint>
 
-#include "nlh_device.h"
+#include "nlh_fast.h"
+#include "nlh_kernel_common.h"
 
 namespace nlh {
 
-// ----------------------------------------------------------------------------
-// helpers
-
-// XCD-aware bijective remap: hardware deals workgroup ids round-robin over
-// the 8 XCDs; give each XCD a contiguous range of work items so that strips
-// sharing halo columns / warm-up rows hit the same L2.
-__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
-  const int q = nwg >> 3, r = nwg & 7, x = bid & 7, l = bid >> 3;
-  return (x < r) ? x * (q + 1) + l : r * (q + 1) + (x - r) * q + l;
-}
-
-__device__ __forceinline__ int find_rect(const RectList &L, int work) {
-  int ri = 0;
-  for (int k = 1; k < L.nrects; ++k) ri = (work >= L.r[k].wg_begin) ? k : ri;
-  return ri;
-}
-
-// floor(sqrt(E^2 - d^2)) == (long)sqrt((double)(E*E - d*d)) of the
-// reference's len_1d_line (:231) for every integer argument < 2^52.
-__host__ __device__ constexpr int clen(int E, int d) {
-  int L = 0;
-  while ((L + 1) * (L + 1) <= E * E - d * d) ++L;
-  return L;
-}
-
-__host__ __device__ constexpr int pow2_ceil(int v) {
-  int p = 1;
-  while (p < v) p <<= 1;
-  return p;
-}
-
-__host__ __device__ constexpr int disk_count(int E) {
-  int n = 0;
-  for (int d = -E; d <= E; ++d) n += 2 * clen(E, d < 0 ? -d : d) + 1;
-  return n;
-}
-
-// One 16-byte-per-lane LDS-DMA: LDS[lds + 16*lane] <- global[g].
-__device__ __forceinline__ void dma16(const void *g, uint32_t lds) {
-  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off"
-               :
-               : "v"(g), "s"(lds)
-               : "memory");
-}
-
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-  static_assert(N >= 0 && N < 64, "vmcnt range");
-  asm volatile("s_waitcnt vmcnt(%0)" : : "n"(N) : "memory");
-}
-
-// NCH 16-byte chunks starting at g -> LDS starting at lds.
-template <int NCH>
-__device__ __forceinline__ void dma_chunks(const double *g, uint32_t lds,
-                                           int lane) {
-#pragma unroll
-  for (int k = 0; k < (NCH + 63) / 64; ++k) {
-    const double *src = g + 2 * (k * 64 + lane);
-    if (k * 64 + 64 <= NCH) {
-      dma16(src, lds + k * 1024);
-    } else if (lane < NCH - k * 64) {
-      dma16(src, lds + k * 1024);
-    }
-  }
-}
-
-__device__ __forceinline__ uint32_t lds_addr(const void *p) {
-  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
-}
 
 // ----------------------------------------------------------------------------
 // k_exact: bit-parity kernel.  64x4 nodes per 256-thread workgroup.
@@ -155,174 +87,6 @@ __global__ __launch_bounds__(256) void k_exact(RectList L, StepConst C) {
     out += r2 * C.dt;
   }
   R.un[(int64_t)y * p + x] = out;
-}
-
-// ----------------------------------------------------------------------------
-// k_fast: nested-window strip sweep.  See the file header.
-//   E  horizon, R columns per lane (strip = 64*R columns), D rows in flight.
-//
-// Per wave: one strip of W = 64*R output columns over one segment of rows.
-// Input rows stream through an LDS ring of K = next_pow2(E+D+1) slots
-// (LDS-DMA issued D rows ahead); a row stays in the ring E rows after its
-// window was consumed, so the centre value u(x, y) of the update is read back
-// from it (slot arithmetic is a mask, no register shifting).  Odd segments sweep upwards
-// so that the 2E rows two neighbouring segments both read are fetched at the
-// same time (L2 hits instead of a second trip to HBM); work items run
-// strip-fastest so horizontally adjacent strips, which share EP halo
-// columns, are co-resident on one XCD.
-template <int E, int R, int D, bool TEST>
-__global__ __launch_bounds__(64) void k_fast(RectList L, StepConst C) {
-  constexpr int P = 2 * E + 1;          // accumulator period (static unroll)
-  constexpr int W = 64 * R;             // strip width (outputs)
-  constexpr int EP = (E + 1) & ~1;      // halo columns staged per side
-  constexpr int RW = W + 2 * EP;        // doubles per ring row
-  constexpr int NCH = RW / 2;           // 16-byte chunks per row
-  constexpr int K = pow2_ceil(E + D + 1);  // ring slots (power of two)
-  constexpr int GU = (NCH + 63) / 64;   // DMA instructions per u row
-  constexpr int GL = TEST ? (W / 2 + 63) / 64 : 0;  // per L_h[W0] row
-  constexpr int G = GU + GL;
-  constexpr int OFF = EP - E;           // window start inside a staged row
-  static_assert(D >= 1, "prefetch distance");
-  static_assert(D * G < 64, "vmcnt range");
-
-  __shared__ __attribute__((aligned(16))) double ring[K * RW + (TEST ? K * W : 0)];
-  double *lwr = ring + K * RW;  // L_h[W0] ring (TEST)
-
-  const int lane = (int)threadIdx.x;
-  const int work = xcd_remap(blockIdx.x, gridDim.x);
-  const int ri = find_rect(L, work);
-  const Rect &Rc = L.r[ri];
-  const int local = work - Rc.wg_begin;
-  const int strip = local % Rc.nstrip, seg = local / Rc.nstrip;
-  const int x0 = Rc.x0 + strip * W;
-  const int Y0 = Rc.y0 + seg * C.seg_h;
-  const int Y1 = min(Y0 + C.seg_h, Rc.y1);
-  const int n_in = (Y1 - Y0) + 2 * E;   // input rows Y0-E .. Y1+E-1
-  const bool up = (seg & 1) != 0;       // sweep direction
-  const int64_t pitch = Rc.pitch;
-  const int64_t stride = up ? -pitch : pitch;
-  const int yfirst = up ? (Y1 + E - 1) : (Y0 - E);  // block-local row of input 0
-
-  const double *g0 = Rc.u + (int64_t)yfirst * pitch + (x0 - EP);
-  // L_h[W0] row of the output emitted at iteration j (j >= 2E): Y0 + j - 2E
-  // sweeping down, Y1 - 1 - (j - 2E) sweeping up
-  const double *l0 = TEST ? Rc.lw + (int64_t)(up ? Y1 - 1 : Y0) * pitch + x0 : nullptr;
-  const uint32_t lring = __builtin_amdgcn_readfirstlane(lds_addr(ring));
-  const uint32_t llw = __builtin_amdgcn_readfirstlane(lds_addr(lwr));
-
-  const int xl = x0 + R * lane;  // first column of this lane
-  double sxv[R];
-  if (TEST) {
-#pragma unroll
-    for (int c = 0; c < R; ++c) {
-      const int xc = min(xl + c, Rc.x1 - 1);
-      sxv[c] = C.sxt[Rc.gx0 + xc + E];
-      asm volatile("" ::"v"(sxv[c]));  // wait for it before the DMA stream
-    }
-  }
-
-  // rows i of the u stream, and L_h rows for the output of iteration i
-  auto issue = [&](int i, int slot) {
-    const int rr = min(i, n_in - 1);
-    dma_chunks<NCH>(g0 + (int64_t)rr * stride, lring + slot * RW * 8, lane);
-    if (TEST) {
-      const int lr = min(max(i - 2 * E, 0), n_in - 2 * E - 1);
-      dma_chunks<W / 2>(l0 + (int64_t)lr * stride, llw + slot * W * 8, lane);
-    }
-  };
-
-#pragma unroll
-  for (int s = 0; s < D; ++s) issue(s, s);
-
-  double acc[R][P];
-#pragma unroll
-  for (int c = 0; c < R; ++c)
-#pragma unroll
-    for (int j = 0; j < P; ++j) acc[c][j] = 0.0;
-  int bs = 0;  // b % K
-  for (int b = 0; b < n_in; b += P) {
-#pragma unroll
-    for (int q = 0; q < P; ++q) {
-      const int i = b + q;
-      if (i < n_in) {
-        const int slot = (bs + q) & (K - 1);
-        issue(i + D, (bs + q + D) & (K - 1));
-        wait_vmcnt<D * G>();
-
-        // window of this lane: columns xl-E .. xl+R-1+E
-        double w[R + 2 * E];
-        const double *rowp = ring + slot * RW;
-        if constexpr (R == 2) {
-          constexpr int NB = (OFF + 2 * E + 2 + 1) / 2;
-          const double2 *rp = reinterpret_cast<const double2 *>(rowp + 2 * lane);
-          double buf[2 * NB];
-#pragma unroll
-          for (int k = 0; k < NB; ++k) {
-            const double2 v = rp[k];
-            buf[2 * k] = v.x;
-            buf[2 * k + 1] = v.y;
-          }
-#pragma unroll
-          for (int k = 0; k < R + 2 * E; ++k) w[k] = buf[OFF + k];
-        } else {
-#pragma unroll
-          for (int k = 0; k < R + 2 * E; ++k) w[k] = rowp[OFF + lane + k];
-        }
-
-        // nested windows + scatter into the accumulators of rows i-d
-#pragma unroll
-        for (int c = 0; c < R; ++c) {
-          double h = w[E + c];
-#pragma unroll
-          for (int Lv = 0; Lv <= E; ++Lv) {
-            if (Lv > 0) h = h + (w[E + c - Lv] + w[E + c + Lv]);
-#pragma unroll
-            for (int d = -E; d <= E; ++d) {
-              if (clen(E, d < 0 ? -d : d) == Lv) acc[c][(q + d + P) % P] += h;
-            }
-          }
-        }
-
-        // output of input row i-E is complete: accumulator (q - E) mod P
-        const int so = (q + E + 1) % P;
-        if (i >= 2 * E) {
-          const int y = up ? (Y1 - 1 - (i - 2 * E)) : (Y0 + i - 2 * E);
-          double out[R];
-          const double *crow = ring + ((bs + q - E) & (K - 1)) * RW + EP + R * lane;
-#pragma unroll
-          for (int c = 0; c < R; ++c) {
-            const double uc = crow[c];
-            const double diff = fma(-C.nf, uc, acc[c][so]);
-            out[c] = fma(diff, C.alpha, uc);
-          }
-          if (TEST) {
-            const double syv = C.syt[Rc.gy0 + y + E];
-            const double *lrow = lwr + slot * W + R * lane;
-#pragma unroll
-            for (int c = 0; c < R; ++c) {
-              const double w0 = sxv[c] * syv;
-              const double bsrc = -(C.st2pi * w0) - C.ct * lrow[c];
-              out[c] = fma(bsrc, C.dt, out[c]);
-            }
-          }
-          double *dst = Rc.un + (int64_t)y * pitch + xl;
-          if constexpr (R == 2) {
-            if (xl + 1 < Rc.x1) {
-              *reinterpret_cast<double2 *>(dst) = make_double2(out[0], out[1]);
-            } else if (xl < Rc.x1) {
-              dst[0] = out[0];
-            }
-          } else {
-            if (xl < Rc.x1) dst[0] = out[0];
-          }
-        }
-#pragma unroll
-        for (int c = 0; c < R; ++c) acc[c][so] = 0.0;
-      }
-    }
-    bs = (bs + P) & (K - 1);
-  }
-  wait_vmcnt<0>();  // drain the clamped tail DMAs before the wave retires
 }
 
 // ----------------------------------------------------------------------------
@@ -404,47 +168,53 @@ static int check_launch() {
   return e == hipSuccess ? 0 : (int)e;
 }
 
-// compile-time dispatch table for the fast kernel: R = 2 (128-column strips)
-// for every E <= 12, R = 4 (256-column strips) for E <= 8.
-constexpr int kFastMaxE = 12;   // E >= 13 spills the accumulator file
-constexpr int kFastMaxE4 = 8;   // widest E with a 256-column variant
-constexpr int kFastD = 6;       // rows in flight per wave
+// Fast-kernel variants, instantiated in nlh_fast_e*.hip (parallel build):
+//   E = 1..16        128-column strips (R = 2); E <= 8 also 256-column (R = 4)
+//   E = 20, 24, 32   64-column strips (R = 1) with the compact centre ring
+// Any other horizon runs k_exact.
+#define NLH_FAST_EXTERN(E, R)                                                            \
+  extern template int launch_fast_er<E, R, true>(const RectList &, const StepConst &, hipStream_t); \
+  extern template int launch_fast_er<E, R, false>(const RectList &, const StepConst &, hipStream_t);
+NLH_FAST_EXTERN(1, 2) NLH_FAST_EXTERN(2, 2) NLH_FAST_EXTERN(3, 2) NLH_FAST_EXTERN(4, 2)
+NLH_FAST_EXTERN(5, 2) NLH_FAST_EXTERN(6, 2) NLH_FAST_EXTERN(7, 2) NLH_FAST_EXTERN(8, 2)
+NLH_FAST_EXTERN(9, 2) NLH_FAST_EXTERN(10, 2) NLH_FAST_EXTERN(11, 2) NLH_FAST_EXTERN(12, 2)
+NLH_FAST_EXTERN(13, 2) NLH_FAST_EXTERN(14, 2) NLH_FAST_EXTERN(15, 2) NLH_FAST_EXTERN(16, 2)
+NLH_FAST_EXTERN(1, 4) NLH_FAST_EXTERN(2, 4) NLH_FAST_EXTERN(3, 4) NLH_FAST_EXTERN(4, 4)
+NLH_FAST_EXTERN(5, 4) NLH_FAST_EXTERN(6, 4) NLH_FAST_EXTERN(7, 4) NLH_FAST_EXTERN(8, 4)
+NLH_FAST_EXTERN(1, 1) NLH_FAST_EXTERN(2, 1) NLH_FAST_EXTERN(3, 1) NLH_FAST_EXTERN(4, 1)
+NLH_FAST_EXTERN(5, 1) NLH_FAST_EXTERN(6, 1) NLH_FAST_EXTERN(7, 1) NLH_FAST_EXTERN(8, 1)
+NLH_FAST_EXTERN(9, 1) NLH_FAST_EXTERN(10, 1) NLH_FAST_EXTERN(11, 1) NLH_FAST_EXTERN(12, 1)
+NLH_FAST_EXTERN(13, 1) NLH_FAST_EXTERN(14, 1) NLH_FAST_EXTERN(15, 1) NLH_FAST_EXTERN(16, 1)
+NLH_FAST_EXTERN(20, 1) NLH_FAST_EXTERN(24, 1) NLH_FAST_EXTERN(32, 1)
 
-template <int E, int R, bool TEST>
-static int launch_fast_er(const RectList &rl, const StepConst &c, hipStream_t st) {
-  hipLaunchKernelGGL((k_fast<E, R, kFastD, TEST>), dim3(rl.nwork), dim3(64), 0, st, rl, c);
-  return check_launch();
+bool fast_supported(int E) { return (E >= 1 && E <= 16) || E == 20 || E == 24 || E == 32; }
+
+int fast_lanes_cols(int E, int want_r) {
+  if (E > 16 || want_r == 1) return 1;
+  return (want_r == 4 && E <= 8) ? 4 : 2;
 }
-
-template <int E>
-static int launch_fast_dispatch(int e, int r, const RectList &rl, const StepConst &c, bool test,
-                                hipStream_t st) {
-  if constexpr (E == 0) {
-    return -1;
-  } else {
-    if (e == E) {
-      if constexpr (E <= kFastMaxE4) {
-        if (r == 4)
-          return test ? launch_fast_er<E, 4, true>(rl, c, st) : launch_fast_er<E, 4, false>(rl, c, st);
-      }
-      return test ? launch_fast_er<E, 2, true>(rl, c, st) : launch_fast_er<E, 2, false>(rl, c, st);
-    }
-    return launch_fast_dispatch<E - 1>(e, r, rl, c, test, st);
-  }
-}
-
-bool fast_supported(int E) { return E >= 1 && (E <= kFastMaxE); }
-
-int fast_lanes_cols(int E, int want_r) { return (want_r == 4 && E <= kFastMaxE4) ? 4 : 2; }
 
 int fast_strip_width(int E, int r) { return 64 * fast_lanes_cols(E, r); }
 
 int fast_seg_min(int E) { return 2 * E; }
 
-int launch_fast(const RectList &rl, const StepConst &c, bool test, int r, void *stream) {
-  if (!fast_supported(c.E)) return -1;
-  return launch_fast_dispatch<kFastMaxE>(c.E, fast_lanes_cols(c.E, r), rl, c, test,
-                                         (hipStream_t)stream);
+int launch_fast(const RectList &rl, const StepConst &c, bool test, int want_r, void *stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const int r = fast_lanes_cols(c.E, want_r);
+#define NLH_CASE(EE, RR)                                                                \
+  if (c.E == EE && r == RR)                                                            \
+    return test ? launch_fast_er<EE, RR, true>(rl, c, st) : launch_fast_er<EE, RR, false>(rl, c, st);
+  NLH_CASE(1, 2) NLH_CASE(2, 2) NLH_CASE(3, 2) NLH_CASE(4, 2) NLH_CASE(5, 2) NLH_CASE(6, 2)
+  NLH_CASE(7, 2) NLH_CASE(8, 2) NLH_CASE(9, 2) NLH_CASE(10, 2) NLH_CASE(11, 2) NLH_CASE(12, 2)
+  NLH_CASE(13, 2) NLH_CASE(14, 2) NLH_CASE(15, 2) NLH_CASE(16, 2)
+  NLH_CASE(1, 4) NLH_CASE(2, 4) NLH_CASE(3, 4) NLH_CASE(4, 4) NLH_CASE(5, 4) NLH_CASE(6, 4)
+  NLH_CASE(7, 4) NLH_CASE(8, 4)
+  NLH_CASE(1, 1) NLH_CASE(2, 1) NLH_CASE(3, 1) NLH_CASE(4, 1) NLH_CASE(5, 1) NLH_CASE(6, 1)
+  NLH_CASE(7, 1) NLH_CASE(8, 1) NLH_CASE(9, 1) NLH_CASE(10, 1) NLH_CASE(11, 1) NLH_CASE(12, 1)
+  NLH_CASE(13, 1) NLH_CASE(14, 1) NLH_CASE(15, 1) NLH_CASE(16, 1)
+  NLH_CASE(20, 1) NLH_CASE(24, 1) NLH_CASE(32, 1)
+#undef NLH_CASE
+  return -1;
 }
 
 int launch_exact(const RectList &rl, const StepConst &c, bool test, void *stream) {

@@ -91,7 +91,10 @@ def test_tiled_rows_single_gpu(oracle, row):
     assert l2 / (r.nx * r.ny) <= 1e-6
 
 
-@pytest.mark.parametrize("eps", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12])
+FAST_EPS = list(range(1, 17)) + [20, 24, 32]
+
+
+@pytest.mark.parametrize("eps", FAST_EPS)
 def test_fast_random_ic_all_eps(oracle, eps):
     rng = np.random.default_rng(12345 + eps)
     nx, ny = 173, 301  # ragged: not multiples of the 128-column strip
@@ -105,3 +108,53 @@ def test_fast_random_ic_all_eps(oracle, eps):
     assert np.max(np.abs(u - u_ref)) <= 1e-12 * scale
     ue, _, _, _ = _gpu_run(r, False, "exact", u0)
     assert np.array_equal(ue, u_ref)
+
+
+@pytest.mark.parametrize("test", [0, 1])
+@pytest.mark.parametrize("kernel", ["exact", "fast"])
+def test_eps32_golden(kernel, test):
+    """96^2, eps=32 (N=3209), 2 steps vs tests/golden/field_eps32_96_test*.npy."""
+    import os
+    from conftest import ROOT
+    g = np.load(os.path.join(ROOT, "tests", "golden", f"field_eps32_96_test{test}.npy"))
+    nx = 96
+    dh = 1.0 / nx
+    dt = 32 ** 4 * dh * dh / (8 * 1.0 * N.disk_count(32))
+    with N.Solver(nx, nx, 32, 1.0, dt, dh, test=bool(test), kernel=kernel) as s:
+        s.test_init()
+        s.run(2)
+        s.synchronize()
+        u = s.field()
+        assert s.info().kernel == (N.KERNEL_EXACT if kernel == "exact" else N.KERNEL_FAST)
+    if kernel == "exact":
+        assert np.array_equal(u, g)
+    else:
+        assert np.max(np.abs(u - g)) <= 1e-12 * np.max(np.abs(g))
+
+
+@pytest.mark.parametrize("eps", [17, 40])
+def test_unsupported_fast_eps_falls_back_to_exact(oracle, eps):
+    r = N.BatchRow(60, 50, 2, eps, 1.0, 1e-4, 1.0 / 60)
+    with N.Solver(r.nx, r.ny, eps, r.k, r.dt, r.dh, test=False, kernel="auto") as s:
+        assert s.info().kernel == N.KERNEL_EXACT
+    with pytest.raises(N.NLHError, match="not instantiated"):
+        N.Solver(r.nx, r.ny, eps, r.k, r.dt, r.dh, test=False, kernel="fast")
+
+
+@pytest.mark.parametrize("r", [1, 2, 4])
+@pytest.mark.parametrize("eps", [3, 8, 12, 16])
+def test_fast_strip_width_variants(oracle, monkeypatch, r, eps):
+    """64-, 128- and 256-column strips (NLH_FAST_R) agree with the oracle."""
+    monkeypatch.setenv("NLH_FAST_R", str(r))
+    rng = np.random.default_rng(99 + eps)
+    nx, ny = 301, 173
+    r_ = N.BatchRow(nx, ny, 4, eps, 1.0, 0.0, 1.0 / nx)
+    r_.dt = eps ** 4 * r_.dh ** 2 / (8 * r_.k * N.disk_count(eps))
+    u0 = rng.uniform(-1.0, 1.0, size=(ny, nx))
+    u_ref, _, _ = _oracle_run(oracle, r_, False, u0)
+    for test in (False, True):
+        if test:
+            u_ref, l2_ref, _ = _oracle_run(oracle, r_, True, u0)
+        u, l2, _, info = _gpu_run(r_, test, "fast", u0)
+        assert info.kernel == N.KERNEL_FAST
+        assert np.max(np.abs(u - u_ref)) <= 1e-12 * np.max(np.abs(u_ref))

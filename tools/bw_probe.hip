@@ -79,6 +79,103 @@ __global__ __launch_bounds__(64) void strip_dma(const double *__restrict__ u, do
   wait_vm<0>();
 }
 
+// same, but the steady state waits with the exact in-order count: every
+// older iteration also issued one store, so D*(2+1) ops are younger than the
+// row being consumed (the warm-up rows, which store nothing, wait for 2*D)
+template <int D>
+__global__ __launch_bounds__(64) void strip_dma_x(const double *__restrict__ u, double *__restrict__ un,
+                                                  int seg_h, int nstrip) {
+  constexpr int RW = 128 + 16, K = D + 1;
+  __shared__ __attribute__((aligned(16))) double ring[K * RW];
+  const int lane = threadIdx.x;
+  const int work = blockIdx.x;
+  const int strip = work % nstrip, seg = work / nstrip;
+  const int x0 = strip * 128, Y0 = seg * seg_h, Y1 = min(Y0 + seg_h, N);
+  const int n_in = Y1 - Y0 + 2 * E;
+  const double *g0 = u + (int64_t)(Y0) * PITCH + XL + x0 - 8;
+  const uint32_t lr = __builtin_amdgcn_readfirstlane(lds_addr(ring));
+  auto issue = [&](int i, int slot) {
+    const int rr = min(i, n_in - 1);
+    const double *g = g0 + (int64_t)rr * PITCH;
+    dma16(g + 2 * lane, lr + slot * RW * 8);
+    if (lane < 8) dma16(g + 128 + 2 * lane, lr + slot * RW * 8 + 1024);
+  };
+  for (int s = 0; s < D; ++s) issue(s, s);
+  int i = 0;
+  for (; i < n_in && i < 2 * E + D; ++i) {
+    issue(i + D, (i + D) % K);
+    wait_vm<2 * D>();
+    const double2 v = *reinterpret_cast<const double2 *>(&ring[(i % K) * RW + 8 + 2 * lane]);
+    if (i >= 2 * E) {
+      const int y = Y0 + i - 2 * E;
+      *reinterpret_cast<double2 *>(un + (int64_t)(y + E) * PITCH + XL + x0 + 2 * lane) = v;
+    }
+  }
+  for (; i < n_in; ++i) {
+    issue(i + D, (i + D) % K);
+    wait_vm<3 * D>();
+    const double2 v = *reinterpret_cast<const double2 *>(&ring[(i % K) * RW + 8 + 2 * lane]);
+    const int y = Y0 + i - 2 * E;
+    *reinterpret_cast<double2 *>(un + (int64_t)(y + E) * PITCH + XL + x0 + 2 * lane) = v;
+  }
+  wait_vm<0>();
+}
+
+// strip/segment order, plain 16-B register loads (no LDS): isolates the
+// access order from the LDS-DMA mechanism
+template <int U>
+__global__ __launch_bounds__(64) void strip_reg(const double *__restrict__ u, double *__restrict__ un,
+                                                int seg_h, int nstrip) {
+  const int lane = threadIdx.x;
+  const int strip = blockIdx.x % nstrip, seg = blockIdx.x / nstrip;
+  const int x0 = strip * 128, Y0 = seg * seg_h, Y1 = min(Y0 + seg_h, N);
+  for (int y = Y0; y < Y1; y += U) {
+    double2 v[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k)
+      v[k] = *reinterpret_cast<const double2 *>(u + (int64_t)(min(y + k, N - 1) + E) * PITCH + XL + x0 + 2 * lane);
+#pragma unroll
+    for (int k = 0; k < U; ++k)
+      if (y + k < Y1)
+        *reinterpret_cast<double2 *>(un + (int64_t)(y + k + E) * PITCH + XL + x0 + 2 * lane) = v[k];
+  }
+}
+
+// strip_dma variants: TAIL = also fetch the 16-double halo tail; NT = nt loads
+template <int D, bool TAIL, bool NT>
+__global__ __launch_bounds__(64) void strip_dma_v(const double *__restrict__ u, double *__restrict__ un,
+                                                  int seg_h, int nstrip) {
+  constexpr int RW = 128 + 16, K = D + 1;
+  __shared__ __attribute__((aligned(16))) double ring[K * RW];
+  const int lane = threadIdx.x;
+  const int strip = blockIdx.x % nstrip, seg = blockIdx.x / nstrip;
+  const int x0 = strip * 128, Y0 = seg * seg_h, Y1 = min(Y0 + seg_h, N);
+  const int n_in = Y1 - Y0 + 2 * E;
+  const double *g0 = u + (int64_t)(Y0) * PITCH + XL + x0 - 8;
+  const uint32_t lr = __builtin_amdgcn_readfirstlane(lds_addr(ring));
+  auto issue = [&](int i, int slot) {
+    const int rr = min(i, n_in - 1);
+    const double *g = g0 + (int64_t)rr * PITCH;
+    if (NT)
+      asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off nt" : : "v"(g + 2 * lane), "s"(lr + slot * RW * 8) : "memory");
+    else
+      dma16(g + 2 * lane, lr + slot * RW * 8);
+    if (TAIL && lane < 8) dma16(g + 128 + 2 * lane, lr + slot * RW * 8 + 1024);
+  };
+  constexpr int G = TAIL ? 2 : 1;
+  for (int s = 0; s < D; ++s) issue(s, s);
+  for (int i = 0; i < n_in; ++i) {
+    issue(i + D, (i + D) % K);
+    wait_vm<G * D>();
+    const double2 v = *reinterpret_cast<const double2 *>(&ring[(i % K) * RW + 8 + 2 * lane]);
+    if (i >= 2 * E) {
+      const int y = Y0 + i - 2 * E;
+      *reinterpret_cast<double2 *>(un + (int64_t)(y + E) * PITCH + XL + x0 + 2 * lane) = v;
+    }
+  }
+  wait_vm<0>();
+}
+
 template <class F>
 static float time_it(F f, int reps) {
   hipEvent_t a, b;
@@ -117,6 +214,27 @@ int main() {
                 "\"us_D12\": %.2f, \"GBps_best\": %.1f}\n",
                 seg, nstrip * nseg, ms4 * 1e3, ms8 * 1e3, ms12 * 1e3,
                 algo / (std::min(ms4, std::min(ms8, ms12)) * 1e-3) / 1e9);
+  }
+  for (int seg : {32, 64, 128, 256}) {
+    const int nseg = (N + seg - 1) / seg;
+    float ms4 = time_it([&] { strip_dma_x<4><<<nstrip * nseg, 64>>>(u, un, seg, nstrip); }, 50);
+    float ms8 = time_it([&] { strip_dma_x<8><<<nstrip * nseg, 64>>>(u, un, seg, nstrip); }, 50);
+    float ms12 = time_it([&] { strip_dma_x<12><<<nstrip * nseg, 64>>>(u, un, seg, nstrip); }, 50);
+    std::printf("{\"variant\": \"strip_dma_exactwait\", \"seg\": %d, \"wgs\": %d, \"us_D4\": %.2f, "
+                "\"us_D8\": %.2f, \"us_D12\": %.2f, \"GBps_best\": %.1f}\n",
+                seg, nstrip * nseg, ms4 * 1e3, ms8 * 1e3, ms12 * 1e3,
+                algo / (std::min(ms4, std::min(ms8, ms12)) * 1e-3) / 1e9);
+  }
+  for (int seg : {64, 128, 256, 4096}) {
+    const int nseg = (N + seg - 1) / seg;
+    float a = time_it([&] { strip_reg<4><<<nstrip * nseg, 64>>>(u, un, seg, nstrip); }, 50);
+    float b = time_it([&] { strip_reg<8><<<nstrip * nseg, 64>>>(u, un, seg, nstrip); }, 50);
+    float c = time_it([&] { strip_dma_v<8, true, false><<<nstrip * nseg, 64>>>(u, un, seg, nstrip); }, 50);
+    float d = time_it([&] { strip_dma_v<8, false, false><<<nstrip * nseg, 64>>>(u, un, seg, nstrip); }, 50);
+    float e = time_it([&] { strip_dma_v<8, true, true><<<nstrip * nseg, 64>>>(u, un, seg, nstrip); }, 50);
+    std::printf("{\"variant\": \"order_vs_mechanism\", \"seg\": %d, \"wgs\": %d, \"reg_U4\": %.2f, "
+                "\"reg_U8\": %.2f, \"dma_tail\": %.2f, \"dma_notail\": %.2f, \"dma_tail_nt\": %.2f}\n",
+                seg, nstrip * nseg, a * 1e3, b * 1e3, c * 1e3, d * 1e3, e * 1e3);
   }
   CK(hipFree(u));
   CK(hipFree(un));
