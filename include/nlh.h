@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define NLH_ABI_VERSION 1
+#define NLH_ABI_VERSION 2
 
 enum nlh_status {
   NLH_OK = 0,
@@ -127,18 +127,22 @@ typedef struct nlh_info {
   int32_t npeers;          /* ranks exchanged with each step               */
   int64_t owned_nodes;     /* nodes owned by this rank                     */
   int64_t disk_points;     /* N(eps): lattice points in the closed disk    */
-  int64_t halo_bytes_sent; /* bytes sent per step to other ranks          */
+  int64_t halo_bytes_sent; /* bytes sent per halo exchange to other ranks */
   int64_t device_bytes;    /* device memory held by the solver             */
   char    arch[32];        /* gcnArchName of the device                    */
+  int32_t halo_width;      /* ghost rows/columns per block: eps, or 2*eps  */
+  int32_t steps_per_pass;  /* 2: production fast mode fuses two steps per
+                              pass over HBM (one halo exchange per pass)   */
 } nlh_info;
 int nlh_get_info(const nlh_solver *s, nlh_info *info);
 
 /* Stencil-kernel timing with HIP events recorded on the stream the stencil
- * kernels are launched on.  While enabled, every stencil launch of nlh_run
- * is bracketed by events; nlh_kernel_time returns the summed duration and the
- * launch count since the last enable.                                      */
+ * kernels are launched on.  While enabled, every stencil pass of nlh_run
+ * (one or two time steps, see nlh_info.steps_per_pass) is bracketed by
+ * events; nlh_kernel_time returns the summed duration and the number of time
+ * steps those passes advanced since the last enable.                      */
 int nlh_kernel_timing(nlh_solver *s, int enable);
-int nlh_kernel_time(nlh_solver *s, double *total_ms, int64_t *launches);
+int nlh_kernel_time(nlh_solver *s, double *total_ms, int64_t *steps);
 
 /* Host-only (no device work): the owner rank of each tile as resolved by the
  * library (reference locidx(), src/2d_nonlocal_distributed.cpp:105-110).  */

@@ -63,7 +63,7 @@ class _Info(ctypes.Structure):
         ("kernel", ctypes.c_int32), ("device", ctypes.c_int32), ("nblocks", ctypes.c_int32),
         ("npeers", ctypes.c_int32), ("owned_nodes", ctypes.c_int64), ("disk_points", ctypes.c_int64),
         ("halo_bytes_sent", ctypes.c_int64), ("device_bytes", ctypes.c_int64),
-        ("arch", ctypes.c_char * 32),
+        ("arch", ctypes.c_char * 32), ("halo_width", ctypes.c_int32), ("steps_per_pass", ctypes.c_int32),
     ]
 
 
@@ -215,6 +215,8 @@ class Info:
     halo_bytes_sent: int
     device_bytes: int
     arch: str
+    halo_width: int = 0
+    steps_per_pass: int = 1
 
 
 class Solver:
@@ -323,12 +325,13 @@ class Solver:
         i = _Info()
         _check(lib().nlh_get_info(self._h, ctypes.byref(i)), "nlh_get_info")
         return Info(i.kernel, i.device, i.nblocks, i.npeers, i.owned_nodes, i.disk_points,
-                    i.halo_bytes_sent, i.device_bytes, i.arch.decode())
+                    i.halo_bytes_sent, i.device_bytes, i.arch.decode(), i.halo_width, i.steps_per_pass)
 
     def kernel_timing(self, enable: bool) -> None:
         _check(lib().nlh_kernel_timing(self._h, int(bool(enable))), "nlh_kernel_timing")
 
     def kernel_time(self):
+        """(summed stencil-pass milliseconds, time steps those passes advanced)."""
         ms = ctypes.c_double()
         n = ctypes.c_int64()
         _check(lib().nlh_kernel_time(self._h, ctypes.byref(ms), ctypes.byref(n)), "nlh_kernel_time")

@@ -85,6 +85,10 @@ struct nlh_solver {
   int device = 0;
   int kernel = NLH_KERNEL_EXACT;
   int fast_r = 2;  // columns per lane of the fast kernel (NLH_FAST_R=1|2|4: 64/128/256-column strips)
+  bool pair = false;  // two steps per pass (nlh_pair.h); production fast mode (NLH_PAIR=0 disables)
+  int halo = 0;       // halo rows/columns held per block: eps, or 2*eps with pair
+  int ablate = 0;     // diagnostics only (NLH_ABLATE), never set in production
+  int pair_ablate = 0;  // diagnostics only (NLH_PAIR_ABLATE)
   hipStream_t s_main = nullptr, s_comm = nullptr;
   hipEvent_t ev_ready = nullptr, ev_halo = nullptr;
   int64_t t = 0;
@@ -96,6 +100,7 @@ struct nlh_solver {
   bool exchange = false;
   // launches per phase and parity (chunked at kMaxRects / kMaxCopies)
   std::vector<nlh::RectList> rl_full[2], rl_int[2], rl_bnd[2];
+  std::vector<nlh::RectList> pl_full[2], pl_int[2], pl_bnd[2];  // pair-kernel launches
   // halo exchange
   ncclComm_t comm = nullptr;
   std::vector<Peer> peers;
@@ -110,6 +115,7 @@ struct nlh_solver {
   bool timing = false;
   std::vector<hipEvent_t> ev_pool;
   size_t ev_used = 0;
+  std::vector<int> ev_steps;  // time steps covered by each timed event pair
   int64_t device_bytes = 0;
   char arch[32] = {0};
 };
@@ -158,15 +164,17 @@ std::vector<LRect> split_block(const LocalBlock &b, int E, int sw) {
   return out;
 }
 
-int build_rectlists(nlh_solver *s) {
+// kind 0: single-step kernels (k_exact / k_fast); kind 1: the pair kernel
+int build_rectlists(nlh_solver *s, int kind) {
   const int E = (int)s->p.eps;
   const bool fast = s->kernel == NLH_KERNEL_FAST;
-  const int sw = fast ? nlh::fast_strip_width(E, s->fast_r) : 64;
-  // gather local rects
+  const bool pair = kind == 1;
+  const int sw = pair ? nlh::pair_strip_width(E) : fast ? nlh::fast_strip_width(E, s->fast_r) : 64;
+  // gather local rects (bands are s->halo wide: what the halo exchange refreshes)
   struct Item { int blk; LRect r; };
   std::vector<Item> all, inter, bnd;
   for (size_t bi = 0; bi < s->blocks.size(); ++bi) {
-    for (auto &r : split_block(s->blocks[bi], E, sw)) {
+    for (auto &r : split_block(s->blocks[bi], s->halo, sw)) {
       Item it{(int)bi, r};
       all.push_back(it);
       (r.interior ? inter : bnd).push_back(it);
@@ -178,10 +186,19 @@ int build_rectlists(nlh_solver *s) {
   if (fast) {
     int64_t strip_rows = 0;
     for (auto &it : all) strip_rows += ceil_div(it.r.x1 - it.r.x0, sw) * (it.r.y1 - it.r.y0);
-    seg_h = s->p.seg_rows > 0 ? s->p.seg_rows
-                              : (int)std::max<int64_t>(nlh::fast_seg_min(E), ceil_div(strip_rows, 1024));
+    const bool own = s->p.seg_rows > 0 && pair == s->pair;  // seg_rows tunes the kernel nlh_run uses most
+    if (pair) {  // 2 waves per SIMD, all resident: 2048 workgroups at most, less one
+                 // per strip column for the per-rect rounding up of segments
+      int64_t strips = 0;
+      for (auto &it : all) strips += ceil_div(it.r.x1 - it.r.x0, sw);
+      const int64_t target = std::max<int64_t>(256, 2048 - strips);
+      seg_h = own ? s->p.seg_rows : (int)std::max<int64_t>(16, ceil_div(strip_rows, target));
+    } else {
+      seg_h = own ? s->p.seg_rows
+                  : (int)std::max<int64_t>(nlh::fast_seg_min(E), ceil_div(strip_rows, 1024));
+    }
   }
-  s->sc.seg_h = seg_h;
+  (pair ? s->sc.seg_pair : s->sc.seg_h) = seg_h;
   auto make = [&](const std::vector<Item> &items, int k, std::vector<nlh::RectList> &out) -> int {
     out.clear();
     int w = 0;
@@ -211,9 +228,9 @@ int build_rectlists(nlh_solver *s) {
   };
   for (int k = 0; k < 2; ++k) {
     int rc;
-    if ((rc = make(all, k, s->rl_full[k])) != NLH_OK) return rc;
-    if ((rc = make(inter, k, s->rl_int[k])) != NLH_OK) return rc;
-    if ((rc = make(bnd, k, s->rl_bnd[k])) != NLH_OK) return rc;
+    if ((rc = make(all, k, pair ? s->pl_full[k] : s->rl_full[k])) != NLH_OK) return rc;
+    if ((rc = make(inter, k, pair ? s->pl_int[k] : s->rl_int[k])) != NLH_OK) return rc;
+    if ((rc = make(bnd, k, pair ? s->pl_bnd[k] : s->rl_bnd[k])) != NLH_OK) return rc;
   }
   return NLH_OK;
 }
@@ -310,11 +327,23 @@ int launch_stencil(nlh_solver *s, const std::vector<nlh::RectList> &v) {
   for (const auto &rl : v) {
     if (rl.nwork == 0) continue;
     int rc;
-    if (s->kernel == NLH_KERNEL_FAST)
+    if (s->kernel == NLH_KERNEL_FAST && !test && s->ablate)
+      rc = nlh::launch_fast_ablation(rl, s->sc, s->ablate, s->s_main);
+    else if (s->kernel == NLH_KERNEL_FAST)
       rc = nlh::launch_fast(rl, s->sc, test, s->fast_r, s->s_main);
     else
       rc = nlh::launch_exact(rl, s->sc, test, s->s_main);
     if (rc != 0) return fail(NLH_ERR_HIP, std::string("stencil launch failed: ") + hipGetErrorString((hipError_t)rc));
+  }
+  return NLH_OK;
+}
+
+int launch_pair_lists(nlh_solver *s, const std::vector<nlh::RectList> &v) {
+  for (const auto &rl : v) {
+    if (rl.nwork == 0) continue;
+    const int rc = s->pair_ablate ? nlh::launch_pair_ablation(rl, s->sc, s->pair_ablate, s->s_main)
+                                  : nlh::launch_pair(rl, s->sc, s->s_main);
+    if (rc != 0) return fail(NLH_ERR_HIP, std::string("pair launch failed: ") + hipGetErrorString((hipError_t)rc));
   }
   return NLH_OK;
 }
@@ -332,18 +361,25 @@ void set_time(nlh_solver *s, int64_t t) {
   s->sc.ct = cos(arg);
 }
 
-int enqueue_step(nlh_solver *s) {
+// one time step (nsteps == 1, k_exact / k_fast) or two (nsteps == 2, the pair
+// kernel): halo exchange on s_comm overlapped with the interior, then the bands
+int enqueue_step(nlh_solver *s, int nsteps) {
   const int k = s->cur;
+  const bool two = nsteps == 2;
   set_time(s, s->t);
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (s->timing) {
     e0 = pool_event(s);
     e1 = pool_event(s);
     if (!e0 || !e1) return fail(NLH_ERR_HIP, "event pool");
+    s->ev_steps.push_back(nsteps);
   }
+  auto stencil = [&](const std::vector<nlh::RectList> &one, const std::vector<nlh::RectList> &pr) {
+    return two ? launch_pair_lists(s, pr) : launch_stencil(s, one);
+  };
   if (!s->exchange) {
     if (e0) HIP_TRY(hipEventRecord(e0, s->s_main));
-    int rc = launch_stencil(s, s->rl_full[k]);
+    int rc = stencil(s->rl_full[k], s->pl_full[k]);
     if (rc) return rc;
     if (e1) HIP_TRY(hipEventRecord(e1, s->s_main));
   } else {
@@ -362,15 +398,15 @@ int enqueue_step(nlh_solver *s) {
     if (launch_copy_lists(s->cl_local[k], s->s_comm)) return NLH_ERR_HIP;
     HIP_TRY(hipEventRecord(s->ev_halo, s->s_comm));
     if (e0) HIP_TRY(hipEventRecord(e0, s->s_main));
-    int rc = launch_stencil(s, s->rl_int[k]);
+    int rc = stencil(s->rl_int[k], s->pl_int[k]);
     if (rc) return rc;
     HIP_TRY(hipStreamWaitEvent(s->s_main, s->ev_halo, 0));
-    rc = launch_stencil(s, s->rl_bnd[k]);
+    rc = stencil(s->rl_bnd[k], s->pl_bnd[k]);
     if (rc) return rc;
     if (e1) HIP_TRY(hipEventRecord(e1, s->s_main));
   }
   s->cur = 1 - k;
-  s->t += 1;
+  s->t += nsteps;
   return NLH_OK;
 }
 
@@ -403,29 +439,29 @@ int compute_lw(nlh_solver *s) {
 
 int destroy_impl(nlh_solver *s) {
   if (!s) return NLH_OK;
-  hipSetDevice(s->device);
-  if (s->s_main) hipStreamSynchronize(s->s_main);
-  if (s->s_comm) hipStreamSynchronize(s->s_comm);
+  (void)hipSetDevice(s->device);
+  if (s->s_main) (void)hipStreamSynchronize(s->s_main);
+  if (s->s_comm) (void)hipStreamSynchronize(s->s_comm);
   if (s->comm) ncclCommDestroy(s->comm);
   for (auto &b : s->blocks) {
-    hipFree(b.base[0]);
-    hipFree(b.base[1]);
-    hipFree(b.lw_base);
+    (void)hipFree(b.base[0]);
+    (void)hipFree(b.base[1]);
+    (void)hipFree(b.lw_base);
   }
   for (auto &pr : s->peers) {
-    hipFree(pr.send);
-    hipFree(pr.recv);
+    (void)hipFree(pr.send);
+    (void)hipFree(pr.recv);
   }
-  hipFree(s->d_sxt);
-  hipFree(s->d_syt);
-  hipFree(s->d_lens);
-  hipFree(s->d_part);
-  hipFree(s->d_red);
-  for (auto e : s->ev_pool) hipEventDestroy(e);
-  if (s->ev_ready) hipEventDestroy(s->ev_ready);
-  if (s->ev_halo) hipEventDestroy(s->ev_halo);
-  if (s->s_main) hipStreamDestroy(s->s_main);
-  if (s->s_comm) hipStreamDestroy(s->s_comm);
+  (void)hipFree(s->d_sxt);
+  (void)hipFree(s->d_syt);
+  (void)hipFree(s->d_lens);
+  (void)hipFree(s->d_part);
+  (void)hipFree(s->d_red);
+  for (auto e : s->ev_pool) (void)hipEventDestroy(e);
+  if (s->ev_ready) (void)hipEventDestroy(s->ev_ready);
+  if (s->ev_halo) (void)hipEventDestroy(s->ev_halo);
+  if (s->s_main) (void)hipStreamDestroy(s->s_main);
+  if (s->s_comm) (void)hipStreamDestroy(s->s_comm);
   delete s;
   return NLH_OK;
 }
@@ -448,7 +484,6 @@ int create_impl(const nlh_params *pin, nlh_solver *s) {
 
   std::string err;
   if (!nlh::resolve_owner(tx, ty, p.nranks, p.owner, s->owner, err)) return fail(NLH_ERR_ARG, err);
-  s->plan = nlh::make_plan(p.nx, p.ny, p.eps, tx, ty, s->owner, p.split_tiles == 0);
 
   // ---- device
   int ndev = 0;
@@ -482,6 +517,16 @@ int create_impl(const nlh_params *pin, nlh_solver *s) {
     s->fast_r = (v == 1 || v == 4) ? v : 2;
   }
   s->fast_r = nlh::fast_lanes_cols(E, s->fast_r);
+  if (const char *ab = std::getenv("NLH_ABLATE")) s->ablate = std::atoi(ab);
+  // production fast mode advances two steps per pass; the source term of the
+  // test mode and a zero alpha (no centre fold) keep the single-step kernels
+  const double alpha = ((p.k * 8) / pow(p.eps * p.dh, 4)) * (p.dh * p.dh) * p.dt;
+  s->pair = kern == NLH_KERNEL_FAST && !p.test && nlh::pair_supported(E) && alpha != 0.0 &&
+            std::isfinite(1.0 / alpha) && s->ablate == 0;
+  if (const char *pe = std::getenv("NLH_PAIR")) s->pair = s->pair && std::atoi(pe) != 0;
+  if (const char *pa = std::getenv("NLH_PAIR_ABLATE")) s->pair_ablate = std::atoi(pa);
+  s->halo = s->pair ? 2 * E : E;
+  s->plan = nlh::make_plan(p.nx, p.ny, s->halo, tx, ty, s->owner, p.split_tiles == 0);
 
   HIP_TRY(hipStreamCreateWithFlags(&s->s_main, hipStreamNonBlocking));
   HIP_TRY(hipStreamCreateWithFlags(&s->s_comm, hipStreamNonBlocking));
@@ -507,6 +552,7 @@ int create_impl(const nlh_params *pin, nlh_solver *s) {
   s->sc.dt = p.dt;
   s->sc.alpha = s->sc.c2d * s->sc.dh2 * p.dt;
   s->sc.nf = (double)s->disk;
+  s->sc.kc = s->pair ? 1.0 / s->sc.alpha - s->sc.nf : 0.0;
   s->sc.sxt = s->d_sxt;
   s->sc.syt = s->d_syt;
   s->sc.lens = s->d_lens;
@@ -516,7 +562,9 @@ int create_impl(const nlh_params *pin, nlh_solver *s) {
   set_time(s, 0);
 
   // ---- local blocks, padded (see nlh_device.h)
-  const int64_t XL = round_up(E, 8);
+  const int64_t XL = round_up(s->halo, 8);
+  int64_t pitch_pad = 0;  // extra doubles per row (layout experiments, NLH_PITCH_PAD)
+  if (const char *pp = std::getenv("NLH_PITCH_PAD")) pitch_pad = 2 * (std::max(0, std::atoi(pp)) / 2);
   for (size_t i = 0; i < s->plan.blocks.size(); ++i) {
     const auto &bd = s->plan.blocks[i];
     if (bd.rank != p.rank) continue;
@@ -524,8 +572,11 @@ int create_impl(const nlh_params *pin, nlh_solver *s) {
     b.plan_index = (int)i;
     b.r = bd.r;
     b.xl = (int32_t)XL;
-    b.pitch = XL + round_up(b.r.w, 256) + XL;  // whole 256-column strips stay in bounds
-    b.rows = b.r.h + 2 * E;
+    // whole 256-column strips stay in bounds; the pair kernel's last strip
+    // stages up to column w + 127
+    const int64_t right = std::max(round_up(b.r.w, 256) + XL, s->pair ? b.r.w + 128 : 0);
+    b.pitch = round_up(XL + right, 8) + pitch_pad;
+    b.rows = b.r.h + 2 * s->halo;
     b.L = b.r.x0 > 0;
     b.Rr = b.r.x0 + b.r.w < p.nx;
     b.T = b.r.y0 > 0;
@@ -544,8 +595,9 @@ int create_impl(const nlh_params *pin, nlh_solver *s) {
     s->blocks.push_back(b);
   }
 
-  int rc = build_rectlists(s);
+  int rc = build_rectlists(s, 0);
   if (rc) return rc;
+  if (s->pair && (rc = build_rectlists(s, 1))) return rc;
 
   // ---- RCCL communicator and exchange plan
   if (p.nranks > 1) {
@@ -730,10 +782,12 @@ int nlh_run(nlh_solver *s, int64_t nsteps) {
   if (nsteps < 0) return fail(NLH_ERR_ARG, "negative step count");
   int rc = set_device(s);
   if (rc) return rc;
-  for (int64_t i = 0; i < nsteps; ++i) {
-    rc = enqueue_step(s);
-    if (rc) return rc;
-  }
+  int64_t i = 0;
+  if (s->pair)
+    for (; i + 2 <= nsteps; i += 2)
+      if ((rc = enqueue_step(s, 2))) return rc;
+  for (; i < nsteps; ++i)
+    if ((rc = enqueue_step(s, 1))) return rc;
   return NLH_OK;
 }
 
@@ -801,6 +855,8 @@ int nlh_get_info(const nlh_solver *s, nlh_info *info) {
   info->disk_points = s->disk;
   info->halo_bytes_sent = s->halo_bytes;
   info->device_bytes = s->device_bytes;
+  info->halo_width = s->halo;
+  info->steps_per_pass = s->pair ? 2 : 1;
   std::snprintf(info->arch, sizeof(info->arch), "%s", s->arch);
   return NLH_OK;
 }
@@ -812,11 +868,12 @@ int nlh_kernel_timing(nlh_solver *s, int enable) {
   HIP_TRY(hipStreamSynchronize(s->s_main));
   s->timing = enable != 0;
   s->ev_used = 0;
+  s->ev_steps.clear();
   return NLH_OK;
 }
 
-int nlh_kernel_time(nlh_solver *s, double *total_ms, int64_t *launches) {
-  if (!s || !total_ms || !launches) return fail(NLH_ERR_ARG, "null argument");
+int nlh_kernel_time(nlh_solver *s, double *total_ms, int64_t *steps_out) {
+  if (!s || !total_ms || !steps_out) return fail(NLH_ERR_ARG, "null argument");
   int rc = set_device(s);
   if (rc) return rc;
   HIP_TRY(hipStreamSynchronize(s->s_main));
@@ -827,7 +884,9 @@ int nlh_kernel_time(nlh_solver *s, double *total_ms, int64_t *launches) {
     tot += ms;
   }
   *total_ms = tot;
-  *launches = (int64_t)(s->ev_used / 2);
+  int64_t steps = 0;
+  for (int n : s->ev_steps) steps += n;
+  *steps_out = steps;
   return NLH_OK;
 }
 

@@ -53,6 +53,9 @@ struct StepConst {
   int64_t nx, ny;  // global lattice
   int32_t E;
   int32_t seg_h;   // fast kernel segment height
+  double kc;       // 1/alpha - N  (pair kernel centre fold)
+  int32_t seg_pair;  // pair kernel segment height
+  int32_t pad_;
 };
 
 // Strided rectangle copy (halo exchange: local block->block copies, pack to
@@ -84,6 +87,14 @@ int fast_strip_width(int E, int want_r);  // 64*R columns per strip
 int fast_seg_min(int E);                  // smallest sensible segment height
 // Work-item counts are filled into rl by the caller (wg_begin/nwork).
 int launch_fast(const RectList &rl, const StepConst &c, bool test, int want_r, void *stream);
+// two waves per (strip, segment), input rows split by parity; production mode
+// two-step pass (nlh_pair.h): production mode, eps in [1, 16]
+bool pair_supported(int E);
+int pair_strip_width(int E);  // output columns per strip: 128 - 2E
+int launch_pair(const RectList &rl, const StepConst &c, void *stream);
+int launch_pair_ablation(const RectList &rl, const StepConst &c, int abl, void *stream);
+// diagnostics (NLH_ABLATE=1|2, eps=8 only): see k_fast's ABL parameter
+int launch_fast_ablation(const RectList &rl, const StepConst &c, int abl, void *stream);
 int launch_exact(const RectList &rl, const StepConst &c, bool test, void *stream);
 // A = sum_local(u) only (no time update) -- used once for L_h[W0].
 int launch_exact_sum(const RectList &rl, const StepConst &c, void *stream);

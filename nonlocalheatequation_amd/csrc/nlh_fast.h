@@ -21,7 +21,12 @@ namespace nlh {
 // columns, are co-resident on one XCD.
 constexpr int kFastD = 6;  // rows in flight per wave
 
-template <int E, int R, int D, bool TEST>
+// ABL (diagnostics only, NLH_ABLATE): bit mask, 0 = production.  1 = no
+// arithmetic (loads/stores kept, window values kept alive), 2 = no HBM traffic
+// (no DMA, no stores), 4 = no XCD remap, 8 = no alternating sweep, 16 = no
+// window LDS reads, 32 = plain (temporal) tail-chunk loads, 64 = plain loads
+// everywhere, 128 = non-temporal stores
+template <int E, int R, int D, bool TEST, int ABL = 0>
 __global__ __launch_bounds__(64) void k_fast(RectList L, StepConst C) {
   constexpr int P = 2 * E + 1;          // accumulator period (static unroll)
   constexpr int W = 64 * R;             // strip width (outputs)
@@ -38,14 +43,17 @@ __global__ __launch_bounds__(64) void k_fast(RectList L, StepConst C) {
   constexpr int G = GU + GL;
   constexpr int OFF = EP - E;           // window start inside a staged row
   static_assert(D >= 1, "prefetch distance");
-  static_assert(D * G < 64, "vmcnt range");
+  // gfx950 counts global stores in vmcnt too: once every one of the last D
+  // iterations has emitted its output row (at least one store instruction each:
+  // lane 0 always owns a column) the wait for row i admits D more ops
+  static_assert(D * G + D < 64, "vmcnt range");
 
   __shared__ __attribute__((aligned(16))) double ring[K * RW + (TEST ? K * W : 0) + (CR ? KC * W : 0)];
   double *lwr = ring + K * RW;                          // L_h[W0] ring (TEST)
   double *cring = ring + K * RW + (TEST ? K * W : 0);   // centre ring (CR)
 
   const int lane = (int)threadIdx.x;
-  const int work = xcd_remap(blockIdx.x, gridDim.x);
+  const int work = (ABL & 4) ? (int)blockIdx.x : xcd_remap(blockIdx.x, gridDim.x);
   const int ri = find_rect(L, work);
   // Rect / StepConst fields in locals (SGPRs): read through the kernarg
   // reference inside the loop they were re-loaded every row
@@ -61,7 +69,7 @@ __global__ __launch_bounds__(64) void k_fast(RectList L, StepConst C) {
   const int Y0 = Rc.y0 + seg * seg_h;
   const int Y1 = min(Y0 + seg_h, Rc.y1);
   const int n_in = (Y1 - Y0) + 2 * E;   // input rows Y0-E .. Y1+E-1
-  const bool up = (seg & 1) != 0;       // sweep direction
+  const bool up = !(ABL & 8) && (seg & 1) != 0;  // sweep direction
   const int64_t pitch = Rc.pitch;
   const int64_t stride = up ? -pitch : pitch;
   const int yfirst = up ? (Y1 + E - 1) : (Y0 - E);  // block-local row of input 0
@@ -90,7 +98,7 @@ __global__ __launch_bounds__(64) void k_fast(RectList L, StepConst C) {
   // the L_h row for the output of iteration i is fetched with row i + D
   const double *gnext = g0;
   auto issue = [&](int i, int slot) {
-    dma_chunks<NCH>(gnext, lring + slot * RW * 8, lane);
+    if (!(ABL & 2)) dma_chunks<NCH, !(ABL & 64), !(ABL & 96)>(gnext, lring + slot * RW * 8, lane);
     if (i + 1 < n_in) gnext += stride;
     if (TEST) {
       const int lr = min(max(i - 2 * E, 0), n_in - 2 * E - 1);
@@ -116,12 +124,18 @@ __global__ __launch_bounds__(64) void k_fast(RectList L, StepConst C) {
       if (i < n_in) {
         const int slot = (bs + q) & (K - 1);
         issue(i + D, (bs + q + D) & (K - 1));
-        wait_vmcnt<D * G>();
+        if (i >= 2 * E + D)
+          wait_vmcnt<D * G + D>();
+        else
+          wait_vmcnt<D * G>();
 
         // window of this lane: columns xl-E .. xl+R-1+E
         double w[R + 2 * E];
         const double *rowp = ring + slot * RW;
-        if constexpr (R % 2 == 0) {  // 16-B aligned: R*lane and the staged row start are even
+        if constexpr ((ABL & 16) != 0) {
+#pragma unroll
+          for (int k = 0; k < R + 2 * E; ++k) w[k] = (double)k;
+        } else if constexpr (R % 2 == 0) {  // 16-B aligned: R*lane and the staged row start are even
           constexpr int NB = (OFF + 2 * E + R + 1) / 2;
           const double2 *rp = reinterpret_cast<const double2 *>(rowp + R * lane);
           double buf[2 * NB];
@@ -143,8 +157,12 @@ __global__ __launch_bounds__(64) void k_fast(RectList L, StepConst C) {
         }
 
         // nested windows + scatter into the accumulators of rows i-d
+        if (ABL & 1) {
 #pragma unroll
-        for (int c = 0; c < R; ++c) {
+          for (int k = 0; k < R + 2 * E; ++k) asm volatile("" ::"v"(w[k]));
+        }
+#pragma unroll
+        for (int c = 0; c < R && !(ABL & 1); ++c) {
           double h = w[E + c];
 #pragma unroll
           for (int Lv = 0; Lv <= E; ++Lv) {
@@ -179,7 +197,19 @@ __global__ __launch_bounds__(64) void k_fast(RectList L, StepConst C) {
               out[c] = fma(bsrc, C.dt, out[c]);
             }
           }
-          if constexpr (R == 2) {
+          if constexpr ((ABL & 2) != 0) {
+#pragma unroll
+            for (int c = 0; c < R; ++c) asm volatile("" ::"v"(out[c]));
+          } else if constexpr ((ABL & 128) != 0 && R == 2) {
+            if (wave_full) {
+              __builtin_nontemporal_store(out[0], dst);
+              __builtin_nontemporal_store(out[1], dst + 1);
+            } else if (xl + 1 < rx1) {
+              *reinterpret_cast<double2 *>(dst) = make_double2(out[0], out[1]);
+            } else if (xl < rx1) {
+              dst[0] = out[0];
+            }
+          } else if constexpr (R == 2) {
             if (wave_full) {
               *reinterpret_cast<double2 *>(dst) = make_double2(out[0], out[1]);
             } else if (xl + 1 < rx1) {
@@ -202,6 +232,13 @@ __global__ __launch_bounds__(64) void k_fast(RectList L, StepConst C) {
     bs = (bs + P) & (K - 1);
   }
   wait_vmcnt<0>();  // drain the clamped tail DMAs before the wave retires
+}
+
+template <int E, int R, int ABL, int D>
+int launch_fast_abl(const RectList &rl, const StepConst &c, hipStream_t st) {
+  hipLaunchKernelGGL((k_fast<E, R, D, false, ABL>), dim3(rl.nwork), dim3(64), 0, st, rl, c);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : (int)e;
 }
 
 template <int E, int R, bool TEST>

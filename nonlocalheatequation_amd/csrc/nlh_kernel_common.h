@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <type_traits>
 
 #include "nlh_device.h"
 
@@ -56,6 +57,13 @@ __device__ __forceinline__ void dma16(const void *g, uint32_t lds) {
                : "memory");
 }
 
+__device__ __forceinline__ void dma16_plain(const void *g, uint32_t lds) {
+  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off"
+               :
+               : "v"(g), "s"(lds)
+               : "memory");
+}
+
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
   static_assert(N >= 0 && N < 64, "vmcnt range");
@@ -63,17 +71,27 @@ __device__ __forceinline__ void wait_vmcnt() {
 }
 
 // NCH 16-byte chunks starting at g -> LDS starting at lds.
-template <int NCH>
+// NTF / NTP: non-temporal hint on the full 64-lane chunks / the partial tail
+template <int NCH, bool NTF = true, bool NTP = true>
 __device__ __forceinline__ void dma_chunks(const double *g, uint32_t lds,
                                            int lane) {
 #pragma unroll
   for (int k = 0; k < (NCH + 63) / 64; ++k) {
     const double *src = g + 2 * (k * 64 + lane);
     if (k * 64 + 64 <= NCH) {
-      dma16(src, lds + k * 1024);
+      if (NTF) dma16(src, lds + k * 1024); else dma16_plain(src, lds + k * 1024);
     } else if (lane < NCH - k * 64) {
-      dma16(src, lds + k * 1024);
+      if (NTP) dma16(src, lds + k * 1024); else dma16_plain(src, lds + k * 1024);
     }
+  }
+}
+
+// f(integral_constant<int, I>) for I = 0 .. N-1, fully unrolled
+template <int N, int I = 0, class F>
+__device__ __forceinline__ void static_for(F &f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<N, I + 1>(f);
   }
 }
 

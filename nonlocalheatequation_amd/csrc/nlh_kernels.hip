@@ -31,6 +31,7 @@
 #include <cstdint>
 
 #include "nlh_fast.h"
+#include "nlh_pair.h"
 #include "nlh_kernel_common.h"
 
 namespace nlh {
@@ -186,6 +187,69 @@ NLH_FAST_EXTERN(5, 1) NLH_FAST_EXTERN(6, 1) NLH_FAST_EXTERN(7, 1) NLH_FAST_EXTER
 NLH_FAST_EXTERN(9, 1) NLH_FAST_EXTERN(10, 1) NLH_FAST_EXTERN(11, 1) NLH_FAST_EXTERN(12, 1)
 NLH_FAST_EXTERN(13, 1) NLH_FAST_EXTERN(14, 1) NLH_FAST_EXTERN(15, 1) NLH_FAST_EXTERN(16, 1)
 NLH_FAST_EXTERN(20, 1) NLH_FAST_EXTERN(24, 1) NLH_FAST_EXTERN(32, 1)
+
+extern template int launch_fast_abl<8, 2, 0, 6>(const RectList &, const StepConst &, hipStream_t);
+extern template int launch_fast_abl<8, 2, 1, 6>(const RectList &, const StepConst &, hipStream_t);
+extern template int launch_fast_abl<8, 2, 2, 6>(const RectList &, const StepConst &, hipStream_t);
+
+// NLH_ABLATE = 100 * k_fast ABL mask + prefetch distance (diagnostics, eps=8, R=2)
+int launch_fast_ablation(const RectList &rl, const StepConst &c, int abl, void *stream) {
+  if (c.E != 8) return -1;
+  hipStream_t st = (hipStream_t)stream;
+  switch (abl) {
+    case 6: return launch_fast_abl<8, 2, 0, 6>(rl, c, st);
+    case 106: return launch_fast_abl<8, 2, 1, 6>(rl, c, st);
+    case 206: return launch_fast_abl<8, 2, 2, 6>(rl, c, st);
+    default: return -1;
+  }
+}
+
+// Two-step pass (nlh_pair.h), instantiated in nlh_pair_e*.hip for E = 1..16
+#define NLH_PAIR_EXTERN(E) \
+  extern template int launch_pair_e<E>(const RectList &, const StepConst &, hipStream_t);
+NLH_PAIR_EXTERN(1) NLH_PAIR_EXTERN(2) NLH_PAIR_EXTERN(3) NLH_PAIR_EXTERN(4)
+NLH_PAIR_EXTERN(5) NLH_PAIR_EXTERN(6) NLH_PAIR_EXTERN(7) NLH_PAIR_EXTERN(8)
+NLH_PAIR_EXTERN(9) NLH_PAIR_EXTERN(10) NLH_PAIR_EXTERN(11) NLH_PAIR_EXTERN(12)
+NLH_PAIR_EXTERN(13) NLH_PAIR_EXTERN(14) NLH_PAIR_EXTERN(15) NLH_PAIR_EXTERN(16)
+
+extern template int launch_pair_abl<8, 2, 6>(const RectList &, const StepConst &, hipStream_t);
+extern template int launch_pair_abl<8, 0, 4>(const RectList &, const StepConst &, hipStream_t);
+extern template int launch_pair_abl<8, 0, 10>(const RectList &, const StepConst &, hipStream_t);
+extern template int launch_pair_abl<8, 0, 14>(const RectList &, const StepConst &, hipStream_t);
+extern template int launch_pair_abl<8, 0, 3>(const RectList &, const StepConst &, hipStream_t);
+
+// NLH_PAIR_ABLATE = 100 * k_pair ABL mask + prefetch distance (diagnostics, eps=8)
+int launch_pair_ablation(const RectList &rl, const StepConst &c, int abl, void *stream) {
+  if (c.E != 8) return -1;
+  hipStream_t st = (hipStream_t)stream;
+  switch (abl) {
+    case 206: return launch_pair_abl<8, 2, 6>(rl, c, st);
+    case 4: return launch_pair_abl<8, 0, 4>(rl, c, st);
+    case 10: return launch_pair_abl<8, 0, 10>(rl, c, st);
+    case 14: return launch_pair_abl<8, 0, 14>(rl, c, st);
+    case 3: return launch_pair_abl<8, 0, 3>(rl, c, st);
+    default: return -1;
+  }
+}
+
+bool pair_supported(int E) { return E >= 1 && E <= 16; }
+
+int pair_strip_width(int E) { return 128 - 2 * E; }
+
+int launch_pair(const RectList &rl, const StepConst &c, void *stream) {
+  hipStream_t st = (hipStream_t)stream;
+  switch (c.E) {
+#define NLH_CASEP(EE) \
+  case EE:            \
+    return launch_pair_e<EE>(rl, c, st);
+    NLH_CASEP(1) NLH_CASEP(2) NLH_CASEP(3) NLH_CASEP(4) NLH_CASEP(5) NLH_CASEP(6)
+    NLH_CASEP(7) NLH_CASEP(8) NLH_CASEP(9) NLH_CASEP(10) NLH_CASEP(11) NLH_CASEP(12)
+    NLH_CASEP(13) NLH_CASEP(14) NLH_CASEP(15) NLH_CASEP(16)
+#undef NLH_CASEP
+    default:
+      return -1;
+  }
+}
 
 bool fast_supported(int E) { return (E >= 1 && E <= 16) || E == 20 || E == 24 || E == 32; }
 

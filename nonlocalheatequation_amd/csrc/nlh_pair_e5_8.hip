@@ -1,0 +1,15 @@
+// nlh_pair_e5_8.hip -- explicit instantiations of the two-step pass (nlh_pair.h)
+// for E = 5..8; split per horizon range so the unrolled kernels compile in parallel.
+#include "nlh_pair.h"
+
+namespace nlh {
+template int launch_pair_e<5>(const RectList &, const StepConst &, hipStream_t);
+template int launch_pair_e<6>(const RectList &, const StepConst &, hipStream_t);
+template int launch_pair_e<7>(const RectList &, const StepConst &, hipStream_t);
+template int launch_pair_e<8>(const RectList &, const StepConst &, hipStream_t);
+template int launch_pair_abl<8, 2, 6>(const RectList &, const StepConst &, hipStream_t);
+template int launch_pair_abl<8, 0, 4>(const RectList &, const StepConst &, hipStream_t);
+template int launch_pair_abl<8, 0, 10>(const RectList &, const StepConst &, hipStream_t);
+template int launch_pair_abl<8, 0, 14>(const RectList &, const StepConst &, hipStream_t);
+template int launch_pair_abl<8, 0, 3>(const RectList &, const StepConst &, hipStream_t);
+}  // namespace nlh

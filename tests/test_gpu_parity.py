@@ -158,3 +158,43 @@ def test_fast_strip_width_variants(oracle, monkeypatch, r, eps):
         u, l2, _, info = _gpu_run(r_, test, "fast", u0)
         assert info.kernel == N.KERNEL_FAST
         assert np.max(np.abs(u - u_ref)) <= 1e-12 * np.max(np.abs(u_ref))
+
+
+@pytest.mark.parametrize("eps", [1, 2, 5, 8, 11, 16])
+@pytest.mark.parametrize("nt", [1, 2, 5])
+def test_pair_pass_matches_oracle(oracle, monkeypatch, eps, nt):
+    """Two-step pass (nlh_pair.h) vs the oracle, and vs the single-step kernel;
+    odd nt ends with one single step.  Ragged sizes cross strip (128-2E) and
+    segment boundaries."""
+    rng = np.random.default_rng(7 + eps)
+    nx, ny = 301, 203
+    r = N.BatchRow(nx, ny, nt, eps, 1.0, 0.0, 1.0 / nx)
+    r.dt = 0.7 * eps ** 4 * r.dh ** 2 / (8 * r.k * N.disk_count(eps))
+    u0 = rng.uniform(-1.0, 1.0, size=(ny, nx))
+    u_ref, _, _ = _oracle_run(oracle, r, False, u0)
+    scale = np.max(np.abs(u_ref))
+    u, _, _, info = _gpu_run(r, False, "fast", u0)
+    assert info.steps_per_pass == 2 and info.halo_width == 2 * eps
+    assert np.max(np.abs(u - u_ref)) <= 1e-12 * scale
+    monkeypatch.setenv("NLH_PAIR", "0")
+    u1, _, _, info1 = _gpu_run(r, False, "fast", u0)
+    assert info1.steps_per_pass == 1 and info1.halo_width == eps
+    assert np.max(np.abs(u1 - u_ref)) <= 1e-12 * scale
+
+
+@pytest.mark.parametrize("seg", [1, 7, 40, 1000])
+def test_pair_segment_heights(oracle, seg):
+    """Segment heights from one row to a whole-strip sweep (seg_rows override)."""
+    rng = np.random.default_rng(seg)
+    nx, ny, eps = 250, 130, 6
+    r = N.BatchRow(nx, ny, 4, eps, 1.0, 0.0, 1.0 / nx)
+    r.dt = 0.9 * eps ** 4 * r.dh ** 2 / (8 * r.k * N.disk_count(eps))
+    u0 = rng.uniform(-1.0, 1.0, size=(ny, nx))
+    u_ref, _, _ = _oracle_run(oracle, r, False, u0)
+    with N.Solver(nx, ny, eps, r.k, r.dt, r.dh, test=False, kernel="fast", seg_rows=seg) as s:
+        s.input_init(u0)
+        s.run(r.nt)
+        s.synchronize()
+        u = s.field()
+        assert s.info().steps_per_pass == 2
+    assert np.max(np.abs(u - u_ref)) <= 1e-12 * np.max(np.abs(u_ref))

@@ -13,6 +13,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #define CK(x)                                                             \
@@ -176,6 +177,18 @@ __global__ __launch_bounds__(64) void strip_dma_v(const double *__restrict__ u, 
   wait_vm<0>();
 }
 
+// random (non-zero, full-entropy mantissa) doubles: HBM power and so
+// throughput depends on the data toggled, a memset-0 buffer flatters a probe
+__global__ void fill_random(double *u, int64_t n) {
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256) {
+    uint64_t z = (uint64_t)e * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    u[e] = (double)(z >> 11) * 0x1.0p-53 - 0.5;
+  }
+}
+
 template <class F>
 static float time_it(F f, int reps) {
   hipEvent_t a, b;
@@ -191,50 +204,47 @@ static float time_it(F f, int reps) {
   return ms / reps;
 }
 
-int main() {
+int main(int argc, char **argv) {
+  const bool full = argc > 1 && std::string(argv[1]) == "--full";
   const size_t bytes = (size_t)PITCH * ROWS * sizeof(double);
   double *u, *un;
   CK(hipMalloc(&u, bytes));
   CK(hipMalloc(&un, bytes));
-  CK(hipMemset(u, 0, bytes));
-  CK(hipMemset(un, 0, bytes));
   const double algo = 16.0 * N * N;
-  for (int g : {1024, 2048, 4096, 8192}) {
-    const float ms = time_it([&] { copy_vec<<<g, 256>>>(u, un); }, 50);
-    std::printf("{\"variant\": \"copy_vec\", \"grid\": %d, \"us\": %.2f, \"GBps\": %.1f}\n", g, ms * 1e3,
-                algo / (ms * 1e-3) / 1e9);
-  }
   const int nstrip = N / 128;
-  for (int seg : {32, 43, 64, 128}) {
-    const int nseg = (N + seg - 1) / seg;
-    float ms4 = time_it([&] { strip_dma<4><<<nstrip * nseg, 64>>>(u, un, seg, nstrip); }, 50);
-    float ms8 = time_it([&] { strip_dma<8><<<nstrip * nseg, 64>>>(u, un, seg, nstrip); }, 50);
-    float ms12 = time_it([&] { strip_dma<12><<<nstrip * nseg, 64>>>(u, un, seg, nstrip); }, 50);
-    std::printf("{\"variant\": \"strip_dma\", \"seg\": %d, \"wgs\": %d, \"us_D4\": %.2f, \"us_D8\": %.2f, "
-                "\"us_D12\": %.2f, \"GBps_best\": %.1f}\n",
-                seg, nstrip * nseg, ms4 * 1e3, ms8 * 1e3, ms12 * 1e3,
-                algo / (std::min(ms4, std::min(ms8, ms12)) * 1e-3) / 1e9);
-  }
-  for (int seg : {32, 64, 128, 256}) {
-    const int nseg = (N + seg - 1) / seg;
-    float ms4 = time_it([&] { strip_dma_x<4><<<nstrip * nseg, 64>>>(u, un, seg, nstrip); }, 50);
-    float ms8 = time_it([&] { strip_dma_x<8><<<nstrip * nseg, 64>>>(u, un, seg, nstrip); }, 50);
-    float ms12 = time_it([&] { strip_dma_x<12><<<nstrip * nseg, 64>>>(u, un, seg, nstrip); }, 50);
-    std::printf("{\"variant\": \"strip_dma_exactwait\", \"seg\": %d, \"wgs\": %d, \"us_D4\": %.2f, "
-                "\"us_D8\": %.2f, \"us_D12\": %.2f, \"GBps_best\": %.1f}\n",
-                seg, nstrip * nseg, ms4 * 1e3, ms8 * 1e3, ms12 * 1e3,
-                algo / (std::min(ms4, std::min(ms8, ms12)) * 1e-3) / 1e9);
-  }
-  for (int seg : {64, 128, 256, 4096}) {
-    const int nseg = (N + seg - 1) / seg;
-    float a = time_it([&] { strip_reg<4><<<nstrip * nseg, 64>>>(u, un, seg, nstrip); }, 50);
-    float b = time_it([&] { strip_reg<8><<<nstrip * nseg, 64>>>(u, un, seg, nstrip); }, 50);
-    float c = time_it([&] { strip_dma_v<8, true, false><<<nstrip * nseg, 64>>>(u, un, seg, nstrip); }, 50);
-    float d = time_it([&] { strip_dma_v<8, false, false><<<nstrip * nseg, 64>>>(u, un, seg, nstrip); }, 50);
-    float e = time_it([&] { strip_dma_v<8, true, true><<<nstrip * nseg, 64>>>(u, un, seg, nstrip); }, 50);
-    std::printf("{\"variant\": \"order_vs_mechanism\", \"seg\": %d, \"wgs\": %d, \"reg_U4\": %.2f, "
-                "\"reg_U8\": %.2f, \"dma_tail\": %.2f, \"dma_notail\": %.2f, \"dma_tail_nt\": %.2f}\n",
-                seg, nstrip * nseg, a * 1e3, b * 1e3, c * 1e3, d * 1e3, e * 1e3);
+  for (int data = 0; data < 2; ++data) {
+    const char *dn = data ? "random" : "zero";
+    if (data) {
+      fill_random<<<4096, 256>>>(u, (int64_t)bytes / 8);
+      fill_random<<<4096, 256>>>(un, (int64_t)bytes / 8);
+    } else {
+      CK(hipMemset(u, 0, bytes));
+      CK(hipMemset(un, 0, bytes));
+    }
+    CK(hipDeviceSynchronize());
+    for (int g : {1024, 8192}) {
+      const float ms = time_it([&] { copy_vec<<<g, 256>>>(u, un); }, 50);
+      std::printf("{\"data\": \"%s\", \"variant\": \"copy_vec\", \"grid\": %d, \"us\": %.2f, \"GBps\": %.1f}\n",
+                  dn, g, ms * 1e3, algo / (ms * 1e-3) / 1e9);
+    }
+    for (int seg : {64, 128, 256}) {
+      const int nseg = (N + seg - 1) / seg;
+      float c = time_it([&] { strip_dma_v<8, true, false><<<nstrip * nseg, 64>>>(u, un, seg, nstrip); }, 50);
+      float e = time_it([&] { strip_dma_v<8, true, true><<<nstrip * nseg, 64>>>(u, un, seg, nstrip); }, 50);
+      std::printf("{\"data\": \"%s\", \"variant\": \"strip_dma\", \"seg\": %d, \"wgs\": %d, "
+                  "\"dma_tail\": %.2f, \"dma_tail_nt\": %.2f}\n", dn, seg, nstrip * nseg, c * 1e3, e * 1e3);
+    }
+    if (!full) continue;
+    for (int seg : {32, 64, 128, 256}) {
+      const int nseg = (N + seg - 1) / seg;
+      float ms4 = time_it([&] { strip_dma_x<4><<<nstrip * nseg, 64>>>(u, un, seg, nstrip); }, 50);
+      float ms8 = time_it([&] { strip_dma_x<8><<<nstrip * nseg, 64>>>(u, un, seg, nstrip); }, 50);
+      float a = time_it([&] { strip_reg<4><<<nstrip * nseg, 64>>>(u, un, seg, nstrip); }, 50);
+      float d = time_it([&] { strip_dma_v<8, false, false><<<nstrip * nseg, 64>>>(u, un, seg, nstrip); }, 50);
+      std::printf("{\"data\": \"%s\", \"variant\": \"detail\", \"seg\": %d, \"exactwait_D4\": %.2f, "
+                  "\"exactwait_D8\": %.2f, \"reg_U4\": %.2f, \"dma_notail\": %.2f}\n",
+                  dn, seg, ms4 * 1e3, ms8 * 1e3, a * 1e3, d * 1e3);
+    }
   }
   CK(hipFree(u));
   CK(hipFree(un));
