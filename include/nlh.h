@@ -137,10 +137,10 @@ typedef struct nlh_info {
 int nlh_get_info(const nlh_solver *s, nlh_info *info);
 
 /* Stencil-kernel timing with HIP events recorded on the stream the stencil
- * kernels are launched on.  While enabled, every stencil pass of nlh_run
- * (one or two time steps, see nlh_info.steps_per_pass) is bracketed by
- * events; nlh_kernel_time returns the summed duration and the number of time
- * steps those passes advanced since the last enable.                      */
+ * kernels are launched on.  While enabled, every nlh_run call is bracketed
+ * by one event pair (its passes run back to back in between; a pass advances
+ * nlh_info.steps_per_pass time steps); nlh_kernel_time returns the summed
+ * duration and the number of time steps advanced since the last enable.   */
 int nlh_kernel_timing(nlh_solver *s, int enable);
 int nlh_kernel_time(nlh_solver *s, double *total_ms, int64_t *steps);
 

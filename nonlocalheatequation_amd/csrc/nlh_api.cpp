@@ -83,6 +83,7 @@ struct nlh_solver {
   nlh::Plan plan;
   std::vector<LocalBlock> blocks;
   int device = 0;
+  int cus = 256;  // compute units of the device
   int kernel = NLH_KERNEL_EXACT;
   int fast_r = 2;  // columns per lane of the fast kernel (NLH_FAST_R=1|2|4: 64/128/256-column strips)
   bool pair = false;  // two steps per pass (nlh_pair.h); production fast mode (NLH_PAIR=0 disables)
@@ -187,11 +188,13 @@ int build_rectlists(nlh_solver *s, int kind) {
     int64_t strip_rows = 0;
     for (auto &it : all) strip_rows += ceil_div(it.r.x1 - it.r.x0, sw) * (it.r.y1 - it.r.y0);
     const bool own = s->p.seg_rows > 0 && pair == s->pair;  // seg_rows tunes the kernel nlh_run uses most
-    if (pair) {  // 2 waves per SIMD, all resident: 2048 workgroups at most, less one
-                 // per strip column for the per-rect rounding up of segments
+    if (pair) {  // one wave per workgroup, all resident at once: at most the
+                 // resident count, less one per strip column for the per-rect
+                 // rounding up of segments
       int64_t strips = 0;
       for (auto &it : all) strips += ceil_div(it.r.x1 - it.r.x0, sw);
-      const int64_t target = std::max<int64_t>(256, 2048 - strips);
+      const int64_t resident = (int64_t)std::max(1, nlh::pair_blocks_per_cu(E)) * s->cus;
+      const int64_t target = std::max<int64_t>(s->cus, resident - strips);
       seg_h = own ? s->p.seg_rows : (int)std::max<int64_t>(16, ceil_div(strip_rows, target));
     } else {
       seg_h = own ? s->p.seg_rows
@@ -367,21 +370,12 @@ int enqueue_step(nlh_solver *s, int nsteps) {
   const int k = s->cur;
   const bool two = nsteps == 2;
   set_time(s, s->t);
-  hipEvent_t e0 = nullptr, e1 = nullptr;
-  if (s->timing) {
-    e0 = pool_event(s);
-    e1 = pool_event(s);
-    if (!e0 || !e1) return fail(NLH_ERR_HIP, "event pool");
-    s->ev_steps.push_back(nsteps);
-  }
   auto stencil = [&](const std::vector<nlh::RectList> &one, const std::vector<nlh::RectList> &pr) {
     return two ? launch_pair_lists(s, pr) : launch_stencil(s, one);
   };
   if (!s->exchange) {
-    if (e0) HIP_TRY(hipEventRecord(e0, s->s_main));
     int rc = stencil(s->rl_full[k], s->pl_full[k]);
     if (rc) return rc;
-    if (e1) HIP_TRY(hipEventRecord(e1, s->s_main));
   } else {
     HIP_TRY(hipEventRecord(s->ev_ready, s->s_main));
     HIP_TRY(hipStreamWaitEvent(s->s_comm, s->ev_ready, 0));
@@ -397,13 +391,11 @@ int enqueue_step(nlh_solver *s, int nsteps) {
     if (launch_copy_lists(s->cl_unpack[k], s->s_comm)) return NLH_ERR_HIP;
     if (launch_copy_lists(s->cl_local[k], s->s_comm)) return NLH_ERR_HIP;
     HIP_TRY(hipEventRecord(s->ev_halo, s->s_comm));
-    if (e0) HIP_TRY(hipEventRecord(e0, s->s_main));
     int rc = stencil(s->rl_int[k], s->pl_int[k]);
     if (rc) return rc;
     HIP_TRY(hipStreamWaitEvent(s->s_main, s->ev_halo, 0));
     rc = stencil(s->rl_bnd[k], s->pl_bnd[k]);
     if (rc) return rc;
-    if (e1) HIP_TRY(hipEventRecord(e1, s->s_main));
   }
   s->cur = 1 - k;
   s->t += nsteps;
@@ -499,6 +491,7 @@ int create_impl(const nlh_params *pin, nlh_solver *s) {
   hipDeviceProp_t prop;
   HIP_TRY(hipGetDeviceProperties(&prop, s->device));
   std::snprintf(s->arch, sizeof(s->arch), "%s", prop.gcnArchName);
+  s->cus = std::max(1, prop.multiProcessorCount);
   if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
     return fail(NLH_ERR_UNSUPPORTED, std::string("libnlh is built for gfx950, device is ") + prop.gcnArchName);
 
@@ -782,12 +775,26 @@ int nlh_run(nlh_solver *s, int64_t nsteps) {
   if (nsteps < 0) return fail(NLH_ERR_ARG, "negative step count");
   int rc = set_device(s);
   if (rc) return rc;
+  if (nsteps == 0) return NLH_OK;
+  // timing: one event pair on the stencil stream around the whole call, so
+  // back-to-back passes are not separated by per-launch event records
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (s->timing) {
+    e0 = pool_event(s);
+    e1 = pool_event(s);
+    if (!e0 || !e1) return fail(NLH_ERR_HIP, "event pool");
+    HIP_TRY(hipEventRecord(e0, s->s_main));
+  }
   int64_t i = 0;
   if (s->pair)
     for (; i + 2 <= nsteps; i += 2)
       if ((rc = enqueue_step(s, 2))) return rc;
   for (; i < nsteps; ++i)
     if ((rc = enqueue_step(s, 1))) return rc;
+  if (e1) {
+    HIP_TRY(hipEventRecord(e1, s->s_main));
+    s->ev_steps.push_back((int)nsteps);
+  }
   return NLH_OK;
 }
 

@@ -87,10 +87,10 @@ int fast_strip_width(int E, int want_r);  // 64*R columns per strip
 int fast_seg_min(int E);                  // smallest sensible segment height
 // Work-item counts are filled into rl by the caller (wg_begin/nwork).
 int launch_fast(const RectList &rl, const StepConst &c, bool test, int want_r, void *stream);
-// two waves per (strip, segment), input rows split by parity; production mode
 // two-step pass (nlh_pair.h): production mode, eps in [1, 16]
 bool pair_supported(int E);
 int pair_strip_width(int E);  // output columns per strip: 128 - 2E
+int pair_blocks_per_cu(int E);  // resident k_pair workgroups per CU (0 = unknown)
 int launch_pair(const RectList &rl, const StepConst &c, void *stream);
 int launch_pair_ablation(const RectList &rl, const StepConst &c, int abl, void *stream);
 // diagnostics (NLH_ABLATE=1|2, eps=8 only): see k_fast's ABL parameter

@@ -206,16 +206,16 @@ int launch_fast_ablation(const RectList &rl, const StepConst &c, int abl, void *
 
 // Two-step pass (nlh_pair.h), instantiated in nlh_pair_e*.hip for E = 1..16
 #define NLH_PAIR_EXTERN(E) \
-  extern template int launch_pair_e<E>(const RectList &, const StepConst &, hipStream_t);
+  extern template int launch_pair_e<E>(const RectList &, const StepConst &, hipStream_t); \
+  extern template int pair_blocks_per_cu_e<E>();
 NLH_PAIR_EXTERN(1) NLH_PAIR_EXTERN(2) NLH_PAIR_EXTERN(3) NLH_PAIR_EXTERN(4)
 NLH_PAIR_EXTERN(5) NLH_PAIR_EXTERN(6) NLH_PAIR_EXTERN(7) NLH_PAIR_EXTERN(8)
 NLH_PAIR_EXTERN(9) NLH_PAIR_EXTERN(10) NLH_PAIR_EXTERN(11) NLH_PAIR_EXTERN(12)
 NLH_PAIR_EXTERN(13) NLH_PAIR_EXTERN(14) NLH_PAIR_EXTERN(15) NLH_PAIR_EXTERN(16)
 
-extern template int launch_pair_abl<8, 2, 6>(const RectList &, const StepConst &, hipStream_t);
-extern template int launch_pair_abl<8, 0, 4>(const RectList &, const StepConst &, hipStream_t);
-extern template int launch_pair_abl<8, 0, 10>(const RectList &, const StepConst &, hipStream_t);
-extern template int launch_pair_abl<8, 0, 14>(const RectList &, const StepConst &, hipStream_t);
+extern template int launch_pair_abl<8, 2, 7>(const RectList &, const StepConst &, hipStream_t);
+extern template int launch_pair_abl<8, 0, 6>(const RectList &, const StepConst &, hipStream_t);
+extern template int launch_pair_abl<8, 0, 5>(const RectList &, const StepConst &, hipStream_t);
 extern template int launch_pair_abl<8, 0, 3>(const RectList &, const StepConst &, hipStream_t);
 
 // NLH_PAIR_ABLATE = 100 * k_pair ABL mask + prefetch distance (diagnostics, eps=8)
@@ -223,10 +223,9 @@ int launch_pair_ablation(const RectList &rl, const StepConst &c, int abl, void *
   if (c.E != 8) return -1;
   hipStream_t st = (hipStream_t)stream;
   switch (abl) {
-    case 206: return launch_pair_abl<8, 2, 6>(rl, c, st);
-    case 4: return launch_pair_abl<8, 0, 4>(rl, c, st);
-    case 10: return launch_pair_abl<8, 0, 10>(rl, c, st);
-    case 14: return launch_pair_abl<8, 0, 14>(rl, c, st);
+    case 207: return launch_pair_abl<8, 2, 7>(rl, c, st);
+    case 6: return launch_pair_abl<8, 0, 6>(rl, c, st);
+    case 5: return launch_pair_abl<8, 0, 5>(rl, c, st);
     case 3: return launch_pair_abl<8, 0, 3>(rl, c, st);
     default: return -1;
   }
@@ -235,6 +234,20 @@ int launch_pair_ablation(const RectList &rl, const StepConst &c, int abl, void *
 bool pair_supported(int E) { return E >= 1 && E <= 16; }
 
 int pair_strip_width(int E) { return 128 - 2 * E; }
+
+int pair_blocks_per_cu(int E) {
+  switch (E) {
+#define NLH_CASEO(EE) \
+  case EE:            \
+    return pair_blocks_per_cu_e<EE>();
+    NLH_CASEO(1) NLH_CASEO(2) NLH_CASEO(3) NLH_CASEO(4) NLH_CASEO(5) NLH_CASEO(6)
+    NLH_CASEO(7) NLH_CASEO(8) NLH_CASEO(9) NLH_CASEO(10) NLH_CASEO(11) NLH_CASEO(12)
+    NLH_CASEO(13) NLH_CASEO(14) NLH_CASEO(15) NLH_CASEO(16)
+#undef NLH_CASEO
+    default:
+      return 0;
+  }
+}
 
 int launch_pair(const RectList &rl, const StepConst &c, void *stream) {
   hipStream_t st = (hipStream_t)stream;

@@ -4,7 +4,11 @@
 
 namespace nlh {
 template int launch_pair_e<13>(const RectList &, const StepConst &, hipStream_t);
+template int pair_blocks_per_cu_e<13>();
 template int launch_pair_e<14>(const RectList &, const StepConst &, hipStream_t);
+template int pair_blocks_per_cu_e<14>();
 template int launch_pair_e<15>(const RectList &, const StepConst &, hipStream_t);
+template int pair_blocks_per_cu_e<15>();
 template int launch_pair_e<16>(const RectList &, const StepConst &, hipStream_t);
+template int pair_blocks_per_cu_e<16>();
 }  // namespace nlh
