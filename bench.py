@@ -151,7 +151,7 @@ def main() -> int:
     # one stencil launch (a "pass") advances steps_per_pass time steps: 2 for
     # the temporally blocked production kernel k_pair, 1 for k_fast / k_exact
     spp = info.steps_per_pass
-    kname = "k_pair" if spp == 2 else ("k_fast" if args.kernel == "fast" else "k_exact")
+    kname = info.pass_kernel
     passes = max(k_n // spp, 1)
     avg_launch_s = (k_ms / 1e3) / passes
     # algorithmic bytes per launch = 16 B per node-update x node-updates of one launch

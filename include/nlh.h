@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define NLH_ABI_VERSION 2
+#define NLH_ABI_VERSION 3
 
 enum nlh_status {
   NLH_OK = 0,
@@ -133,6 +133,8 @@ typedef struct nlh_info {
   int32_t halo_width;      /* ghost rows/columns per block: eps, or 2*eps  */
   int32_t steps_per_pass;  /* 2: production fast mode fuses two steps per
                               pass over HBM (one halo exchange per pass)   */
+  char    pass_kernel[32]; /* device kernel of one full pass: "k_pair_split",
+                              "k_pair_mw", "k_pair", "k_fast" or "k_exact"  */
 } nlh_info;
 int nlh_get_info(const nlh_solver *s, nlh_info *info);
 

@@ -64,6 +64,7 @@ class _Info(ctypes.Structure):
         ("npeers", ctypes.c_int32), ("owned_nodes", ctypes.c_int64), ("disk_points", ctypes.c_int64),
         ("halo_bytes_sent", ctypes.c_int64), ("device_bytes", ctypes.c_int64),
         ("arch", ctypes.c_char * 32), ("halo_width", ctypes.c_int32), ("steps_per_pass", ctypes.c_int32),
+        ("pass_kernel", ctypes.c_char * 32),
     ]
 
 
@@ -217,6 +218,7 @@ class Info:
     arch: str
     halo_width: int = 0
     steps_per_pass: int = 1
+    pass_kernel: str = ""
 
 
 class Solver:
@@ -325,7 +327,8 @@ class Solver:
         i = _Info()
         _check(lib().nlh_get_info(self._h, ctypes.byref(i)), "nlh_get_info")
         return Info(i.kernel, i.device, i.nblocks, i.npeers, i.owned_nodes, i.disk_points,
-                    i.halo_bytes_sent, i.device_bytes, i.arch.decode(), i.halo_width, i.steps_per_pass)
+                    i.halo_bytes_sent, i.device_bytes, i.arch.decode(), i.halo_width, i.steps_per_pass,
+                    i.pass_kernel.decode())
 
     def kernel_timing(self, enable: bool) -> None:
         _check(lib().nlh_kernel_timing(self._h, int(bool(enable))), "nlh_kernel_timing")

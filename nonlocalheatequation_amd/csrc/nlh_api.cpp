@@ -90,6 +90,7 @@ struct nlh_solver {
   int halo = 0;       // halo rows/columns held per block: eps, or 2*eps with pair
   int ablate = 0;     // diagnostics only (NLH_ABLATE), never set in production
   int pair_ablate = 0;  // diagnostics only (NLH_PAIR_ABLATE)
+  int pair_split = 1;  // 1 k_pair_split (default), 0 k_pair, 2 k_pair_mw (NLH_PAIR_SPLIT)
   hipStream_t s_main = nullptr, s_comm = nullptr;
   hipEvent_t ev_ready = nullptr, ev_halo = nullptr;
   int64_t t = 0;
@@ -193,7 +194,11 @@ int build_rectlists(nlh_solver *s, int kind) {
                  // rounding up of segments
       int64_t strips = 0;
       for (auto &it : all) strips += ceil_div(it.r.x1 - it.r.x0, sw);
-      const int64_t resident = (int64_t)std::max(1, nlh::pair_blocks_per_cu(E)) * s->cus;
+      // k_pair: every resident wave (2 per SIMD at E = 8); k_pair_split: 4
+      // workgroups (8 waves) per CU -- taller segments beat more waves
+      // (profiles/r01/pair_v3)
+      const int per_cu = std::max(1, nlh::pair_blocks_per_cu(E, s->pair_split));
+      const int64_t resident = (int64_t)(s->pair_split != 0 ? std::min(per_cu, 4) : per_cu) * s->cus;
       const int64_t target = std::max<int64_t>(s->cus, resident - strips);
       seg_h = own ? s->p.seg_rows : (int)std::max<int64_t>(16, ceil_div(strip_rows, target));
     } else {
@@ -345,7 +350,7 @@ int launch_pair_lists(nlh_solver *s, const std::vector<nlh::RectList> &v) {
   for (const auto &rl : v) {
     if (rl.nwork == 0) continue;
     const int rc = s->pair_ablate ? nlh::launch_pair_ablation(rl, s->sc, s->pair_ablate, s->s_main)
-                                  : nlh::launch_pair(rl, s->sc, s->s_main);
+                                  : nlh::launch_pair(rl, s->sc, s->pair_split, s->s_main);
     if (rc != 0) return fail(NLH_ERR_HIP, std::string("pair launch failed: ") + hipGetErrorString((hipError_t)rc));
   }
   return NLH_OK;
@@ -518,6 +523,8 @@ int create_impl(const nlh_params *pin, nlh_solver *s) {
             std::isfinite(1.0 / alpha) && s->ablate == 0;
   if (const char *pe = std::getenv("NLH_PAIR")) s->pair = s->pair && std::atoi(pe) != 0;
   if (const char *pa = std::getenv("NLH_PAIR_ABLATE")) s->pair_ablate = std::atoi(pa);
+  if (const char *ps = std::getenv("NLH_PAIR_SPLIT")) s->pair_split = std::min(2, std::max(0, std::atoi(ps)));
+  if (s->pair_ablate >= 10000) s->pair_split = 1;
   s->halo = s->pair ? 2 * E : E;
   s->plan = nlh::make_plan(p.nx, p.ny, s->halo, tx, ty, s->owner, p.split_tiles == 0);
 
@@ -864,6 +871,9 @@ int nlh_get_info(const nlh_solver *s, nlh_info *info) {
   info->device_bytes = s->device_bytes;
   info->halo_width = s->halo;
   info->steps_per_pass = s->pair ? 2 : 1;
+  const char *pk = s->pair ? (s->pair_split == 2 ? "k_pair_mw" : s->pair_split == 1 ? "k_pair_split" : "k_pair")
+                           : (s->kernel == NLH_KERNEL_FAST ? "k_fast" : "k_exact");
+  std::snprintf(info->pass_kernel, sizeof(info->pass_kernel), "%s", pk);
   std::snprintf(info->arch, sizeof(info->arch), "%s", s->arch);
   return NLH_OK;
 }

@@ -90,8 +90,10 @@ int launch_fast(const RectList &rl, const StepConst &c, bool test, int want_r, v
 // two-step pass (nlh_pair.h): production mode, eps in [1, 16]
 bool pair_supported(int E);
 int pair_strip_width(int E);  // output columns per strip: 128 - 2E
-int pair_blocks_per_cu(int E);  // resident k_pair workgroups per CU (0 = unknown)
-int launch_pair(const RectList &rl, const StepConst &c, void *stream);
+// variant: 0 k_pair (one wave), 1 k_pair_split (the two stages on two
+// waves), 2 k_pair_mw (plus a third wave for all HBM traffic)
+int pair_blocks_per_cu(int E, int variant);  // resident workgroups per CU (0 = unknown)
+int launch_pair(const RectList &rl, const StepConst &c, int variant, void *stream);
 int launch_pair_ablation(const RectList &rl, const StepConst &c, int abl, void *stream);
 // diagnostics (NLH_ABLATE=1|2, eps=8 only): see k_fast's ABL parameter
 int launch_fast_ablation(const RectList &rl, const StepConst &c, int abl, void *stream);

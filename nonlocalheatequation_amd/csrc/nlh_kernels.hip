@@ -206,8 +206,8 @@ int launch_fast_ablation(const RectList &rl, const StepConst &c, int abl, void *
 
 // Two-step pass (nlh_pair.h), instantiated in nlh_pair_e*.hip for E = 1..16
 #define NLH_PAIR_EXTERN(E) \
-  extern template int launch_pair_e<E>(const RectList &, const StepConst &, hipStream_t); \
-  extern template int pair_blocks_per_cu_e<E>();
+  extern template int launch_pair_e<E>(const RectList &, const StepConst &, int, hipStream_t); \
+  extern template int pair_blocks_per_cu_e<E>(int);
 NLH_PAIR_EXTERN(1) NLH_PAIR_EXTERN(2) NLH_PAIR_EXTERN(3) NLH_PAIR_EXTERN(4)
 NLH_PAIR_EXTERN(5) NLH_PAIR_EXTERN(6) NLH_PAIR_EXTERN(7) NLH_PAIR_EXTERN(8)
 NLH_PAIR_EXTERN(9) NLH_PAIR_EXTERN(10) NLH_PAIR_EXTERN(11) NLH_PAIR_EXTERN(12)
@@ -218,7 +218,13 @@ extern template int launch_pair_abl<8, 0, 6>(const RectList &, const StepConst &
 extern template int launch_pair_abl<8, 0, 5>(const RectList &, const StepConst &, hipStream_t);
 extern template int launch_pair_abl<8, 0, 3>(const RectList &, const StepConst &, hipStream_t);
 
-// NLH_PAIR_ABLATE = 100 * k_pair ABL mask + prefetch distance (diagnostics, eps=8)
+extern template int launch_pair_abl<8, 2, 8, true, 4>(const RectList &, const StepConst &, hipStream_t);
+extern template int launch_pair_abl<8, 0, 6, true, 1>(const RectList &, const StepConst &, hipStream_t);
+extern template int launch_pair_abl<8, 0, 6, true, 2>(const RectList &, const StepConst &, hipStream_t);
+extern template int launch_pair_abl<8, 0, 6, true, 4>(const RectList &, const StepConst &, hipStream_t);
+extern template int launch_pair_abl<8, 0, 10, true, 2>(const RectList &, const StepConst &, hipStream_t);
+// NLH_PAIR_ABLATE = 100 * k_pair ABL mask + prefetch distance (diagnostics, eps=8);
+// >= 10000: k_pair_split, 10000 + 1000 * ABL + 100 * B + D
 int launch_pair_ablation(const RectList &rl, const StepConst &c, int abl, void *stream) {
   if (c.E != 8) return -1;
   hipStream_t st = (hipStream_t)stream;
@@ -227,19 +233,27 @@ int launch_pair_ablation(const RectList &rl, const StepConst &c, int abl, void *
     case 6: return launch_pair_abl<8, 0, 6>(rl, c, st);
     case 5: return launch_pair_abl<8, 0, 5>(rl, c, st);
     case 3: return launch_pair_abl<8, 0, 3>(rl, c, st);
+    case 12408: return launch_pair_abl<8, 2, 8, true, 4>(rl, c, st);
+    case 10106: return launch_pair_abl<8, 0, 6, true, 1>(rl, c, st);
+    case 10206: return launch_pair_abl<8, 0, 6, true, 2>(rl, c, st);
+    case 10406: return launch_pair_abl<8, 0, 6, true, 4>(rl, c, st);
+    case 10210: return launch_pair_abl<8, 0, 10, true, 2>(rl, c, st);
     default: return -1;
   }
 }
 
-bool pair_supported(int E) { return E >= 1 && E <= 16; }
+// E = 13 and 15 spill registers in k_pair_split under hipcc 7.2 (and k_pair
+// runs one wave per SIMD there): the single-step k_fast is faster for them
+// (profiles/r01/pair_v4/tune_eps_split.jsonl)
+bool pair_supported(int E) { return (E >= 1 && E <= 12) || E == 14 || E == 16; }
 
 int pair_strip_width(int E) { return 128 - 2 * E; }
 
-int pair_blocks_per_cu(int E) {
+int pair_blocks_per_cu(int E, int variant) {
   switch (E) {
 #define NLH_CASEO(EE) \
   case EE:            \
-    return pair_blocks_per_cu_e<EE>();
+    return pair_blocks_per_cu_e<EE>(variant);
     NLH_CASEO(1) NLH_CASEO(2) NLH_CASEO(3) NLH_CASEO(4) NLH_CASEO(5) NLH_CASEO(6)
     NLH_CASEO(7) NLH_CASEO(8) NLH_CASEO(9) NLH_CASEO(10) NLH_CASEO(11) NLH_CASEO(12)
     NLH_CASEO(13) NLH_CASEO(14) NLH_CASEO(15) NLH_CASEO(16)
@@ -249,12 +263,12 @@ int pair_blocks_per_cu(int E) {
   }
 }
 
-int launch_pair(const RectList &rl, const StepConst &c, void *stream) {
+int launch_pair(const RectList &rl, const StepConst &c, int variant, void *stream) {
   hipStream_t st = (hipStream_t)stream;
   switch (c.E) {
 #define NLH_CASEP(EE) \
   case EE:            \
-    return launch_pair_e<EE>(rl, c, st);
+    return launch_pair_e<EE>(rl, c, variant, st);
     NLH_CASEP(1) NLH_CASEP(2) NLH_CASEP(3) NLH_CASEP(4) NLH_CASEP(5) NLH_CASEP(6)
     NLH_CASEP(7) NLH_CASEP(8) NLH_CASEP(9) NLH_CASEP(10) NLH_CASEP(11) NLH_CASEP(12)
     NLH_CASEP(13) NLH_CASEP(14) NLH_CASEP(15) NLH_CASEP(16)

@@ -41,7 +41,10 @@
 
 namespace nlh {
 
-constexpr int kPairD = 7;  // u^t rows in flight per wave (ring of 8 slots)
+constexpr int kPairD = 7;       // k_pair: u^t rows in flight per wave (ring of 8 slots)
+constexpr int kPairSplitD = 8;  // k_pair_split: rows in flight beyond the next block
+constexpr int kPairSplitB = 4;  // k_pair_split: rows per barrier
+constexpr int kPairMwD = 6;     // k_pair_mw: rows in flight beyond the next block
 
 // some row offset d of the disk has half-width len(d) == L
 __host__ __device__ constexpr bool pair_level_used(int E, int L) {
@@ -252,9 +255,376 @@ __global__ __launch_bounds__(64, (E <= 9 ? 2 : 1)) void k_pair(RectList L, StepC
   wait_vmcnt<0>();  // drain the clamped tail DMAs before the wave retires
 }
 
-template <int E, int ABL, int D = kPairD>
+// k_pair_split: the two stages of k_pair on the two waves of one workgroup,
+// synchronised once per block of B rows (s_barrier):
+//   wave 0 (stage 1): u^t row i from the LDS ring -> u^{t+1} row i-2E into a
+//                     2B-row LDS ring;
+//   wave 1 (memory + stage 2): LDS-DMA of u^t row i+B+D (and, at each block
+//                     end, the wait for the next block's rows, so wave 0
+//                     never waits on HBM), stage 2 on u^{t+1} row i-2E-B (the
+//                     block wave 0 finished before the last barrier), and the
+//                     u^{t+2} store.
+// Each wave holds ONE accumulator set (2 x (2E+1) doubles): at the two waves
+// per SIMD of k_pair a workgroup owns a segment twice as tall, so less of the
+// 4E / 2E rows of redundant halo work per segment (4 workgroups per CU
+// measured best, see nlh_api.cpp); one barrier per B rows lets per-row
+// jitter of the two waves average out.  Same arithmetic and order as
+// k_pair: bitwise equal results.
+template <int E, int D, int ABL = 0, int B = kPairSplitB>
+__global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) {
+  constexpr int R = 2;
+  constexpr int P = 2 * E + 1;
+  constexpr int W1 = 64 * R;
+  constexpr int WO = W1 - 2 * E;
+  constexpr int NW = R + 2 * E;
+  constexpr int RW = W1 + 2 * E;
+  constexpr int NCH = RW / 2;
+  constexpr int DT = B + D;             // rows fetched ahead of wave 0's row
+  constexpr int K = pow2_ceil(DT + B);  // rows i .. i+DT+B-1 live at once
+  constexpr int G = (NCH + 63) / 64;
+  constexpr int U1W = W1 + 2 * E + 2;
+  constexpr int U1R = 2 * B;            // u^{t+1} ring rows
+  static_assert((B & (B - 1)) == 0, "B must be a power of two");
+  static_assert(D * G + D + 1 < 64, "vmcnt range");
+  static_assert(WO >= 64, "strip too narrow for this eps");
+
+  __shared__ __attribute__((aligned(16))) double ring[K * RW + U1R * U1W];
+  double *const u1buf = ring + K * RW;
+
+  const int lane = (int)(threadIdx.x & 63);
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int work = xcd_remap(blockIdx.x, gridDim.x);
+  const int ri = find_rect(L, work);
+  const Rect &Rc = L.r[ri];
+  const int rx1 = Rc.x1, rgx0 = Rc.gx0, rgy0 = Rc.gy0;
+  const int local = work - Rc.wg_begin;
+  const int nstrip = Rc.nstrip;
+  const int strip = local % nstrip, seg = local / nstrip;
+  const int x0 = Rc.x0 + strip * WO;
+  const int seg_h = C.seg_pair;
+  const int Y0 = Rc.y0 + seg * seg_h;
+  const int Y1 = min(Y0 + seg_h, Rc.y1);
+  const int n_in = (Y1 - Y0) + 4 * E;   // u^t rows Y0-2E .. Y1+2E-1
+  const int i_last = n_in - 1 + B;      // wave 1's last iteration
+  const bool up = (seg & 1) != 0;
+  const int64_t pitch = Rc.pitch;
+  const int64_t stride = up ? -pitch : pitch;
+  const double alpha = C.alpha, kc = C.kc;
+  const int ydir = up ? -1 : 1;
+
+  // s_barrier with every LDS access of this wave completed first; the asm
+  // "memory" clobber also keeps the compiler from moving LDS accesses across
+  auto row_barrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+
+  double acc[R][P];
+#pragma unroll
+  for (int c = 0; c < R; ++c)
+#pragma unroll
+    for (int j = 0; j < P; ++j) acc[c][j] = 0.0;
+
+  // barriers: one prologue barrier, then one after every iteration i with
+  // i % B == B-1, for i = 0 .. i_last (wave 0 stops computing at n_in - 1)
+  if (wave == 0) {
+    // ---- stage 1 on u^t row i
+    const int gny = (int)C.ny;
+    const int gy1first = rgy0 + (up ? (Y1 + E - 1) : (Y0 - E));
+    double mcol[R];
+#pragma unroll
+    for (int c = 0; c < R; ++c) {
+      const int gx = rgx0 + x0 - E + R * lane + c;
+      mcol[c] = (gx >= 0 && gx < (int)C.nx) ? alpha : 0.0;
+    }
+    row_barrier();  // prologue: rows 0 .. B-1 landed
+    int bs = 0;     // b % K
+    for (int b = 0; b < n_in; b += P) {
+      auto body = [&](auto qc) {
+        constexpr int q = decltype(qc)::value;
+        constexpr int so = (q + E + 1) % P;
+        const int i = b + q;
+        if (i >= n_in) return;
+        double w[NW];
+        pair_window<E, R>(ring + ((bs + q) & (K - 1)) * RW + R * lane, w);
+        pair_scatter<E, q>(w, acc, kc);
+        if (i >= 2 * E) {
+          const int m = i - 2 * E;
+          const int gy = gy1first + ydir * m;
+          double v0 = mcol[0] * acc[0][so];
+          double v1 = mcol[1] * acc[1][so];
+          if (gy < 0 || gy >= gny) {
+            v0 = 0.0;
+            v1 = 0.0;
+          }
+          *reinterpret_cast<double2 *>(u1buf + (m & (U1R - 1)) * U1W + R * lane) = make_double2(v0, v1);
+        }
+        if ((i & (B - 1)) == B - 1) row_barrier();
+      };
+      static_for<P>(body);
+      bs = (bs + P) & (K - 1);
+    }
+    // the block-end barriers of wave 1's iterations n_in .. i_last
+    for (int j = (i_last + 1) / B - n_in / B; j > 0; --j) row_barrier();
+  } else {
+    // ---- memory + stage 2 on u^{t+1} row m2 = i - 2E - B
+    const int yfirst = up ? (Y1 + 2 * E - 1) : (Y0 - 2 * E);
+    const double *gnext = Rc.u + (int64_t)yfirst * pitch + (x0 - 2 * E);
+    const uint32_t lring = __builtin_amdgcn_readfirstlane(lds_addr(ring));
+    int row = 0;  // next u^t row to fetch (clamped at the last one)
+    auto issue = [&](int slot) {
+      if (!(ABL & 2)) dma_chunks<NCH>(gnext, lring + slot * RW * 8, lane);
+      if (++row < n_in) gnext += stride;
+    };
+#pragma unroll
+    for (int s = 0; s < DT; ++s) issue(s);
+    wait_vmcnt<D * G>();  // rows 0 .. B-1 landed (D rows may still fly)
+    row_barrier();
+    const int xo = x0 + R * lane;
+    const bool emit0 = R * lane < WO && xo < rx1;
+    const bool emit1 = R * lane < WO && xo + 1 < rx1;
+    double *const run = Rc.un;
+    const int yout0 = up ? Y1 - 1 : Y0;
+    // block end at iteration j: wave 0 next reads rows j+1 .. j+B, so row
+    // j+B (issued first thing in iteration j+B-DT = j-D) must have landed.
+    // Issued after it: the DMAs of iterations j-D+1 .. j (D*G) and the
+    // stores of iterations j-D .. j (at least one each once stores have
+    // begun, iteration 4E+B; more outstanding only makes the wait longer)
+    auto block_end = [&](int j) {
+      if ((j & (B - 1)) != B - 1) return;
+      if (j - D >= 4 * E + B)
+        wait_vmcnt<D * G + D + 1>();
+      else
+        wait_vmcnt<D * G>();
+      row_barrier();
+    };
+    // iterations 0 .. P-1 have no u^{t+1} row yet (m2 < 0; n_in > P always):
+    // fetch + barrier only.  Peeled, so the accumulators never sit under a
+    // branch (a conditional scatter makes the compiler copy them around)
+    for (int i = 0; i < P; ++i) {
+      issue((i + DT) & (K - 1));
+      block_end(i);
+    }
+    int bs = P & (K - 1);  // b % K
+    for (int b = P; b <= i_last; b += P) {
+      auto body = [&](auto qc) {
+        constexpr int q = decltype(qc)::value;
+        constexpr int q2 = ((q + 1 - B) % P + P) % P;  // slot of row m2 = i - 2E - B
+        constexpr int so = (q2 + E + 1) % P;
+        const int i = b + q;
+        if (i > i_last) return;
+        issue((bs + q + DT) & (K - 1));  // u^t row i+DT (clamped; never a slot wave 0 still reads)
+        // u^{t+1} row m2 = i - 2E - B (m2 mod P == q2); rows m2 < 0 are LDS
+        // garbage that only reaches accumulators of rows never emitted, each
+        // assigned afresh before use
+        const int m2 = i - 2 * E - B;
+        double w2[NW];
+        pair_window<E, R>(u1buf + (m2 & (U1R - 1)) * U1W + R * lane, w2);
+        pair_scatter<E, q2>(w2, acc, kc);
+        if (m2 >= 2 * E) {
+          const double o0 = alpha * acc[0][so];
+          const double o1 = alpha * acc[1][so];
+          double *dst = run + (int64_t)(yout0 + ydir * (m2 - 2 * E)) * pitch;
+          if constexpr ((ABL & 2) != 0) {
+            asm volatile("" ::"v"(o0), "v"(o1));
+          } else if (emit1) {
+            *reinterpret_cast<double2 *>(dst + xo) = make_double2(o0, o1);
+          } else if (emit0) {
+            dst[xo] = o0;
+          }
+        }
+        block_end(i);
+      };
+      static_for<P>(body);
+      bs = (bs + P) & (K - 1);
+    }
+    wait_vmcnt<0>();  // drain the clamped tail DMAs and the stores
+  }
+}
+
+// k_pair_mw: k_pair_split with all HBM traffic on a third wave, so the two
+// arithmetic waves never issue a global memory instruction:
+//   wave 0: stage 1 (as k_pair_split);
+//   wave 1: stage 2, u^{t+2} rows into a 2B-row LDS output ring;
+//   wave 2: LDS-DMA of u^t rows (and the block-end waits), and the copy of
+//           each finished u^{t+2} row LDS -> HBM one block after wave 1 wrote
+//           it.
+// Barriers at every block end of iterations 0 .. n_in-1+2B (+ one prologue
+// barrier), all three waves.  Bitwise equal to k_pair_split.
+template <int E, int D, int ABL = 0, int B = 2>
+__global__ __launch_bounds__(192, 3) void k_pair_mw(RectList L, StepConst C) {
+  constexpr int R = 2;
+  constexpr int P = 2 * E + 1;
+  constexpr int W1 = 64 * R;
+  constexpr int WO = W1 - 2 * E;
+  constexpr int NW = R + 2 * E;
+  constexpr int RW = W1 + 2 * E;
+  constexpr int NCH = RW / 2;
+  constexpr int DT = B + D;
+  constexpr int K = pow2_ceil(DT + B);
+  constexpr int G = (NCH + 63) / 64;
+  constexpr int U1W = W1 + 2 * E + 2;
+  constexpr int U1R = 2 * B;
+  static_assert((B & (B - 1)) == 0, "B must be a power of two");
+  static_assert(D * G + D + 1 < 64, "vmcnt range");
+  static_assert(WO >= 64, "strip too narrow for this eps");
+
+  __shared__ __attribute__((aligned(16))) double ring[K * RW + U1R * U1W + U1R * W1];
+  double *const u1buf = ring + K * RW;
+  double *const obuf = u1buf + U1R * U1W;
+
+  const int lane = (int)(threadIdx.x & 63);
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int work = xcd_remap(blockIdx.x, gridDim.x);
+  const int ri = find_rect(L, work);
+  const Rect &Rc = L.r[ri];
+  const int rx1 = Rc.x1, rgx0 = Rc.gx0, rgy0 = Rc.gy0;
+  const int local = work - Rc.wg_begin;
+  const int nstrip = Rc.nstrip;
+  const int strip = local % nstrip, seg = local / nstrip;
+  const int x0 = Rc.x0 + strip * WO;
+  const int seg_h = C.seg_pair;
+  const int Y0 = Rc.y0 + seg * seg_h;
+  const int Y1 = min(Y0 + seg_h, Rc.y1);
+  const int n_in = (Y1 - Y0) + 4 * E;
+  const int i_last = n_in - 1 + B;      // wave 1's last iteration
+  const int i_end = i_last + B;         // wave 2's last iteration
+  const int nbar = (i_end + 1) / B;     // block-end barriers of iterations 0 .. i_end
+  const bool up = (seg & 1) != 0;
+  const int64_t pitch = Rc.pitch;
+  const int64_t stride = up ? -pitch : pitch;
+  const double alpha = C.alpha, kc = C.kc;
+  const int ydir = up ? -1 : 1;
+
+  auto row_barrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+
+  if (wave == 0) {
+    // ---- stage 1 on u^t row i (as k_pair_split)
+    double acc[R][P];
+#pragma unroll
+    for (int c = 0; c < R; ++c)
+#pragma unroll
+      for (int j = 0; j < P; ++j) acc[c][j] = 0.0;
+    const int gny = (int)C.ny;
+    const int gy1first = rgy0 + (up ? (Y1 + E - 1) : (Y0 - E));
+    double mcol[R];
+#pragma unroll
+    for (int c = 0; c < R; ++c) {
+      const int gx = rgx0 + x0 - E + R * lane + c;
+      mcol[c] = (gx >= 0 && gx < (int)C.nx) ? alpha : 0.0;
+    }
+    row_barrier();
+    int bs = 0;
+    for (int b = 0; b < n_in; b += P) {
+      auto body = [&](auto qc) {
+        constexpr int q = decltype(qc)::value;
+        constexpr int so = (q + E + 1) % P;
+        const int i = b + q;
+        if (i >= n_in) return;
+        double w[NW];
+        pair_window<E, R>(ring + ((bs + q) & (K - 1)) * RW + R * lane, w);
+        pair_scatter<E, q>(w, acc, kc);
+        if (i >= 2 * E) {
+          const int m = i - 2 * E;
+          const int gy = gy1first + ydir * m;
+          double v0 = mcol[0] * acc[0][so];
+          double v1 = mcol[1] * acc[1][so];
+          if (gy < 0 || gy >= gny) {
+            v0 = 0.0;
+            v1 = 0.0;
+          }
+          *reinterpret_cast<double2 *>(u1buf + (m & (U1R - 1)) * U1W + R * lane) = make_double2(v0, v1);
+        }
+        if ((i & (B - 1)) == B - 1) row_barrier();
+      };
+      static_for<P>(body);
+      bs = (bs + P) & (K - 1);
+    }
+    for (int j = nbar - n_in / B; j > 0; --j) row_barrier();
+  } else if (wave == 1) {
+    // ---- stage 2 on u^{t+1} row m2 = i - 2E - B; u^{t+2} row k = m2 - 2E
+    // into the output ring
+    double acc[R][P];
+#pragma unroll
+    for (int c = 0; c < R; ++c)
+#pragma unroll
+      for (int j = 0; j < P; ++j) acc[c][j] = 0.0;
+    row_barrier();
+    for (int i = 0; i < P; ++i)
+      if ((i & (B - 1)) == B - 1) row_barrier();
+    for (int b = P; b <= i_last; b += P) {
+      auto body = [&](auto qc) {
+        constexpr int q = decltype(qc)::value;
+        constexpr int q2 = ((q + 1 - B) % P + P) % P;
+        constexpr int so = (q2 + E + 1) % P;
+        const int i = b + q;
+        if (i > i_last) return;
+        const int m2 = i - 2 * E - B;
+        double w2[NW];
+        pair_window<E, R>(u1buf + (m2 & (U1R - 1)) * U1W + R * lane, w2);
+        pair_scatter<E, q2>(w2, acc, kc);
+        if (m2 >= 2 * E) {
+          const int k = m2 - 2 * E;
+          *reinterpret_cast<double2 *>(obuf + (k & (U1R - 1)) * W1 + R * lane) =
+              make_double2(alpha * acc[0][so], alpha * acc[1][so]);
+        }
+        if ((i & (B - 1)) == B - 1) row_barrier();
+      };
+      static_for<P>(body);
+    }
+    for (int j = nbar - (i_last + 1) / B; j > 0; --j) row_barrier();
+  } else {
+    // ---- memory: u^t rows in, u^{t+2} rows out
+    const int yfirst = up ? (Y1 + 2 * E - 1) : (Y0 - 2 * E);
+    const double *gnext = Rc.u + (int64_t)yfirst * pitch + (x0 - 2 * E);
+    const uint32_t lring = __builtin_amdgcn_readfirstlane(lds_addr(ring));
+    int row = 0;
+    auto issue = [&](int slot) {
+      if (!(ABL & 2)) dma_chunks<NCH>(gnext, lring + slot * RW * 8, lane);
+      if (++row < n_in) gnext += stride;
+    };
+#pragma unroll
+    for (int s = 0; s < DT; ++s) issue(s);
+    wait_vmcnt<D * G>();
+    row_barrier();
+    const int xo = x0 + R * lane;
+    const bool emit0 = R * lane < WO && xo < rx1;
+    const bool emit1 = R * lane < WO && xo + 1 < rx1;
+    double *const run = Rc.un;
+    const int yout0 = up ? Y1 - 1 : Y0;
+    const int nout = Y1 - Y0;
+    for (int i = 0; i <= i_end; ++i) {
+      issue((i + DT) & (K - 1));
+      // u^{t+2} row k finished by wave 1 one block ago
+      const int k = i - 4 * E - 2 * B;
+      if (k >= 0 && k < nout) {
+        const double2 o = *reinterpret_cast<const double2 *>(obuf + (k & (U1R - 1)) * W1 + R * lane);
+        double *dst = run + (int64_t)(yout0 + ydir * k) * pitch;
+        if constexpr ((ABL & 2) != 0) {
+          asm volatile("" ::"v"(o.x), "v"(o.y));
+        } else if (emit1) {
+          *reinterpret_cast<double2 *>(dst + xo) = o;
+        } else if (emit0) {
+          dst[xo] = o.x;
+        }
+      }
+      if ((i & (B - 1)) == B - 1) {
+        // row i+B (issued in iteration i-D) landed; after it: D*G DMAs and
+        // the stores of iterations i-D .. i (stores from iteration 4E+2B on)
+        if (i - D >= 4 * E + 2 * B)
+          wait_vmcnt<D * G + D + 1>();
+        else
+          wait_vmcnt<D * G>();
+        row_barrier();
+      }
+    }
+    wait_vmcnt<0>();
+  }
+}
+
+template <int E, int ABL, int D = kPairD, bool SPLIT = false, int B = kPairSplitB>
 int launch_pair_abl(const RectList &rl, const StepConst &c, hipStream_t st) {
-  hipLaunchKernelGGL((k_pair<E, D, ABL>), dim3(rl.nwork), dim3(64), 0, st, rl, c);
+  if constexpr (SPLIT)
+    hipLaunchKernelGGL((k_pair_split<E, D, ABL, B>), dim3(rl.nwork), dim3(128), 0, st, rl, c);
+  else
+    hipLaunchKernelGGL((k_pair<E, D, ABL>), dim3(rl.nwork), dim3(64), 0, st, rl, c);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : (int)e;
 }
@@ -262,15 +632,23 @@ int launch_pair_abl(const RectList &rl, const StepConst &c, hipStream_t st) {
 // resident k_pair workgroups per CU (register/LDS-limited), for the
 // host's choice of segment height
 template <int E>
-int pair_blocks_per_cu_e() {
+int pair_blocks_per_cu_e(int variant) {
   int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_pair<E, kPairD>, 64, 0) != hipSuccess) return 0;
-  return n;
+  const hipError_t e =
+      variant == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_pair_mw<E, kPairMwD>, 192, 0)
+      : variant == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_pair_split<E, kPairSplitD>, 128, 0)
+                     : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_pair<E, kPairD>, 64, 0);
+  return e == hipSuccess ? n : 0;
 }
 
 template <int E>
-int launch_pair_e(const RectList &rl, const StepConst &c, hipStream_t st) {
-  hipLaunchKernelGGL((k_pair<E, kPairD>), dim3(rl.nwork), dim3(64), 0, st, rl, c);
+int launch_pair_e(const RectList &rl, const StepConst &c, int variant, hipStream_t st) {
+  if (variant == 2)
+    hipLaunchKernelGGL((k_pair_mw<E, kPairMwD>), dim3(rl.nwork), dim3(192), 0, st, rl, c);
+  else if (variant == 1)
+    hipLaunchKernelGGL((k_pair_split<E, kPairSplitD>), dim3(rl.nwork), dim3(128), 0, st, rl, c);
+  else
+    hipLaunchKernelGGL((k_pair<E, kPairD>), dim3(rl.nwork), dim3(64), 0, st, rl, c);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : (int)e;
 }

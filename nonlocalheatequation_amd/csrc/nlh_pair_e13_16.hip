@@ -3,12 +3,12 @@
 #include "nlh_pair.h"
 
 namespace nlh {
-template int launch_pair_e<13>(const RectList &, const StepConst &, hipStream_t);
-template int pair_blocks_per_cu_e<13>();
-template int launch_pair_e<14>(const RectList &, const StepConst &, hipStream_t);
-template int pair_blocks_per_cu_e<14>();
-template int launch_pair_e<15>(const RectList &, const StepConst &, hipStream_t);
-template int pair_blocks_per_cu_e<15>();
-template int launch_pair_e<16>(const RectList &, const StepConst &, hipStream_t);
-template int pair_blocks_per_cu_e<16>();
+template int launch_pair_e<13>(const RectList &, const StepConst &, int, hipStream_t);
+template int pair_blocks_per_cu_e<13>(int);
+template int launch_pair_e<14>(const RectList &, const StepConst &, int, hipStream_t);
+template int pair_blocks_per_cu_e<14>(int);
+template int launch_pair_e<15>(const RectList &, const StepConst &, int, hipStream_t);
+template int pair_blocks_per_cu_e<15>(int);
+template int launch_pair_e<16>(const RectList &, const StepConst &, int, hipStream_t);
+template int pair_blocks_per_cu_e<16>(int);
 }  // namespace nlh

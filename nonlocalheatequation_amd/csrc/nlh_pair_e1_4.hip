@@ -3,12 +3,12 @@
 #include "nlh_pair.h"
 
 namespace nlh {
-template int launch_pair_e<1>(const RectList &, const StepConst &, hipStream_t);
-template int pair_blocks_per_cu_e<1>();
-template int launch_pair_e<2>(const RectList &, const StepConst &, hipStream_t);
-template int pair_blocks_per_cu_e<2>();
-template int launch_pair_e<3>(const RectList &, const StepConst &, hipStream_t);
-template int pair_blocks_per_cu_e<3>();
-template int launch_pair_e<4>(const RectList &, const StepConst &, hipStream_t);
-template int pair_blocks_per_cu_e<4>();
+template int launch_pair_e<1>(const RectList &, const StepConst &, int, hipStream_t);
+template int pair_blocks_per_cu_e<1>(int);
+template int launch_pair_e<2>(const RectList &, const StepConst &, int, hipStream_t);
+template int pair_blocks_per_cu_e<2>(int);
+template int launch_pair_e<3>(const RectList &, const StepConst &, int, hipStream_t);
+template int pair_blocks_per_cu_e<3>(int);
+template int launch_pair_e<4>(const RectList &, const StepConst &, int, hipStream_t);
+template int pair_blocks_per_cu_e<4>(int);
 }  // namespace nlh

@@ -3,12 +3,12 @@
 #include "nlh_pair.h"
 
 namespace nlh {
-template int launch_pair_e<9>(const RectList &, const StepConst &, hipStream_t);
-template int pair_blocks_per_cu_e<9>();
-template int launch_pair_e<10>(const RectList &, const StepConst &, hipStream_t);
-template int pair_blocks_per_cu_e<10>();
-template int launch_pair_e<11>(const RectList &, const StepConst &, hipStream_t);
-template int pair_blocks_per_cu_e<11>();
-template int launch_pair_e<12>(const RectList &, const StepConst &, hipStream_t);
-template int pair_blocks_per_cu_e<12>();
+template int launch_pair_e<9>(const RectList &, const StepConst &, int, hipStream_t);
+template int pair_blocks_per_cu_e<9>(int);
+template int launch_pair_e<10>(const RectList &, const StepConst &, int, hipStream_t);
+template int pair_blocks_per_cu_e<10>(int);
+template int launch_pair_e<11>(const RectList &, const StepConst &, int, hipStream_t);
+template int pair_blocks_per_cu_e<11>(int);
+template int launch_pair_e<12>(const RectList &, const StepConst &, int, hipStream_t);
+template int pair_blocks_per_cu_e<12>(int);
 }  // namespace nlh

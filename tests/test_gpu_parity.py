@@ -198,3 +198,32 @@ def test_pair_segment_heights(oracle, seg):
         u = s.field()
         assert s.info().steps_per_pass == 2
     assert np.max(np.abs(u - u_ref)) <= 1e-12 * np.max(np.abs(u_ref))
+
+
+@pytest.mark.parametrize("eps", [3, 8, 12, 16])
+def test_pair_split_bitwise_equals_one_wave_pair(monkeypatch, eps):
+    """k_pair_split (stages on two waves), k_pair_mw (plus a memory wave) and
+    k_pair (one wave) run the same arithmetic in the same order: bitwise
+    equal at equal segmentation."""
+    rng = np.random.default_rng(3 + eps)
+    nx, ny = 257, 190
+    dh = 1.0 / nx
+    dt = 0.8 * eps ** 4 * dh * dh / (8 * N.disk_count(eps))
+    u0 = rng.uniform(-1.0, 1.0, size=(ny, nx))
+    out = {}
+    for split in ("1", "0", "2"):
+        monkeypatch.setenv("NLH_PAIR_SPLIT", split)
+        with N.Solver(nx, ny, eps, 1.0, dt, dh, test=False, kernel="fast", seg_rows=37) as s:
+            s.input_init(u0)
+            s.run(6)
+            s.synchronize()
+            out[split] = s.field()
+            assert s.info().steps_per_pass == 2
+    assert np.array_equal(out["1"].view(np.uint64), out["0"].view(np.uint64))
+    assert np.array_equal(out["2"].view(np.uint64), out["0"].view(np.uint64))
+
+
+@pytest.mark.parametrize("eps", [13, 15])
+def test_pair_not_used_where_single_step_is_faster(eps):
+    with N.Solver(300, 200, eps, 1.0, 1e-9, 1.0 / 300, test=False, kernel="fast") as s:
+        assert s.info().steps_per_pass == 1 and s.info().halo_width == eps
