@@ -91,8 +91,10 @@ struct nlh_solver {
   int ablate = 0;     // diagnostics only (NLH_ABLATE), never set in production
   int pair_ablate = 0;  // diagnostics only (NLH_PAIR_ABLATE)
   int pair_split = 1;  // 1 k_pair_split (default), 0 k_pair, 2 k_pair_mw (NLH_PAIR_SPLIT)
-  hipStream_t s_main = nullptr, s_comm = nullptr;
-  hipEvent_t ev_ready = nullptr, ev_halo = nullptr;
+  hipStream_t s_main = nullptr, s_comm = nullptr, s_band = nullptr;
+  hipEvent_t ev_ready = nullptr, ev_halo = nullptr, ev_band = nullptr, ev_int = nullptr;
+  bool halo_fresh = false;  // the current field's halo holds its neighbours' values
+  bool force_bands = false;  // diagnostics (NLH_FORCE_BANDS): exchange-path schedule on one block
   int64_t t = 0;
   int cur = 0;
   double *d_sxt = nullptr, *d_syt = nullptr;
@@ -207,6 +209,19 @@ int build_rectlists(nlh_solver *s, int kind) {
     }
   }
   (pair ? s->sc.seg_pair : s->sc.seg_h) = seg_h;
+  // halo bands run beside the interior kernel (enqueue_step); their segments
+  // are short -- about one band workgroup per CU -- so that bands, the
+  // exchange they feed and the next pass's bands fit inside one interior
+  // pass.  NLH_BAND_SEG overrides the height (diagnostics)
+  int seg_band = seg_h;
+  if (fast) {
+    int64_t band_rows = 0;
+    for (auto &it : bnd) band_rows += ceil_div(it.r.x1 - it.r.x0, sw) * (it.r.y1 - it.r.y0);
+    const int lo = std::min(seg_h, 2 * E);
+    seg_band = (int)std::min<int64_t>(seg_h, std::max<int64_t>(lo, ceil_div(band_rows, (int64_t)s->cus)));
+    if (const char *bsg = std::getenv("NLH_BAND_SEG"))
+      if (std::atoi(bsg) > 0) seg_band = std::atoi(bsg);
+  }
   auto make = [&](const std::vector<Item> &items, int k, std::vector<nlh::RectList> &out) -> int {
     out.clear();
     int w = 0;
@@ -222,8 +237,9 @@ int build_rectlists(nlh_solver *s, int kind) {
       fill_rect_common(R, s->blocks[it.blk], k, s);
       R.x0 = it.r.x0; R.y0 = it.r.y0; R.x1 = it.r.x1; R.y1 = it.r.y1;
       if (fast) {
+        R.seg_rows = it.r.interior ? seg_h : seg_band;
         R.nstrip = (int)ceil_div(R.x1 - R.x0, sw);
-        R.nseg = (int)ceil_div(R.y1 - R.y0, seg_h);
+        R.nseg = (int)ceil_div(R.y1 - R.y0, R.seg_rows);
       } else {
         R.nstrip = (int)ceil_div(R.x1 - R.x0, 64);
         R.nseg = (int)ceil_div(R.y1 - R.y0, 4);
@@ -317,7 +333,7 @@ int build_exchange(nlh_solver *s) {
     }
   }
   for (auto &kv : peers) s->peers.push_back(kv.second);
-  s->exchange = !s->plan.pieces.empty();
+  s->exchange = !s->plan.pieces.empty() || s->force_bands;
   return NLH_OK;
 }
 
@@ -330,27 +346,27 @@ hipEvent_t pool_event(nlh_solver *s) {
   return s->ev_pool[s->ev_used++];
 }
 
-int launch_stencil(nlh_solver *s, const std::vector<nlh::RectList> &v) {
+int launch_stencil(nlh_solver *s, const std::vector<nlh::RectList> &v, hipStream_t st) {
   const bool test = s->p.test != 0;
   for (const auto &rl : v) {
     if (rl.nwork == 0) continue;
     int rc;
     if (s->kernel == NLH_KERNEL_FAST && !test && s->ablate)
-      rc = nlh::launch_fast_ablation(rl, s->sc, s->ablate, s->s_main);
+      rc = nlh::launch_fast_ablation(rl, s->sc, s->ablate, st);
     else if (s->kernel == NLH_KERNEL_FAST)
-      rc = nlh::launch_fast(rl, s->sc, test, s->fast_r, s->s_main);
+      rc = nlh::launch_fast(rl, s->sc, test, s->fast_r, st);
     else
-      rc = nlh::launch_exact(rl, s->sc, test, s->s_main);
+      rc = nlh::launch_exact(rl, s->sc, test, st);
     if (rc != 0) return fail(NLH_ERR_HIP, std::string("stencil launch failed: ") + hipGetErrorString((hipError_t)rc));
   }
   return NLH_OK;
 }
 
-int launch_pair_lists(nlh_solver *s, const std::vector<nlh::RectList> &v) {
+int launch_pair_lists(nlh_solver *s, const std::vector<nlh::RectList> &v, hipStream_t st) {
   for (const auto &rl : v) {
     if (rl.nwork == 0) continue;
-    const int rc = s->pair_ablate ? nlh::launch_pair_ablation(rl, s->sc, s->pair_ablate, s->s_main)
-                                  : nlh::launch_pair(rl, s->sc, s->pair_split, s->s_main);
+    const int rc = s->pair_ablate ? nlh::launch_pair_ablation(rl, s->sc, s->pair_ablate, st)
+                                  : nlh::launch_pair(rl, s->sc, s->pair_split, st);
     if (rc != 0) return fail(NLH_ERR_HIP, std::string("pair launch failed: ") + hipGetErrorString((hipError_t)rc));
   }
   return NLH_OK;
@@ -369,38 +385,60 @@ void set_time(nlh_solver *s, int64_t t) {
   s->sc.ct = cos(arg);
 }
 
+// halo exchange of the field in buffer parity k on the comm stream: pack the
+// pieces other ranks need -> grouped ncclSend / ncclRecv per peer -> unpack
+// + local block-to-block copies; records ev_halo
+int enqueue_exchange(nlh_solver *s, int k) {
+  if (launch_copy_lists(s->cl_pack[k], s->s_comm)) return NLH_ERR_HIP;
+  if (!s->peers.empty()) {
+    NCCL_TRY(ncclGroupStart());
+    for (auto &pr : s->peers) {
+      if (pr.send_count) NCCL_TRY(ncclSend(pr.send, pr.send_count, ncclDouble, pr.rank, s->comm, s->s_comm));
+      if (pr.recv_count) NCCL_TRY(ncclRecv(pr.recv, pr.recv_count, ncclDouble, pr.rank, s->comm, s->s_comm));
+    }
+    NCCL_TRY(ncclGroupEnd());
+  }
+  if (launch_copy_lists(s->cl_unpack[k], s->s_comm)) return NLH_ERR_HIP;
+  if (launch_copy_lists(s->cl_local[k], s->s_comm)) return NLH_ERR_HIP;
+  HIP_TRY(hipEventRecord(s->ev_halo, s->s_comm));
+  return NLH_OK;
+}
+
 // one time step (nsteps == 1, k_exact / k_fast) or two (nsteps == 2, the pair
-// kernel): halo exchange on s_comm overlapped with the interior, then the bands
+// kernel).  With an exchange (several blocks / ranks), pass n runs
+//   s_band : wait halo(n) and interior(n-1); bands(n)    (nodes within the
+//            halo width of a block edge: they read the halo)
+//   s_main : wait bands(n-1); interior(n)                (concurrently)
+//   s_comm : wait bands(n); exchange -> halo(n+1)        (overlaps interior(n))
+// so the exchange of the next pass's halo overlaps this pass's interior, and
+// the bands -- short segments, see build_rectlists -- run beside it.  The
+// pieces sent are band nodes only (every node within the halo width of a
+// block side that is not on the domain boundary belongs to a band).
 int enqueue_step(nlh_solver *s, int nsteps) {
   const int k = s->cur;
   const bool two = nsteps == 2;
   set_time(s, s->t);
-  auto stencil = [&](const std::vector<nlh::RectList> &one, const std::vector<nlh::RectList> &pr) {
-    return two ? launch_pair_lists(s, pr) : launch_stencil(s, one);
-  };
+  auto stencil = [&](const std::vector<nlh::RectList> &one, const std::vector<nlh::RectList> &pr,
+                     hipStream_t st) { return two ? launch_pair_lists(s, pr, st) : launch_stencil(s, one, st); };
+  int rc;
   if (!s->exchange) {
-    int rc = stencil(s->rl_full[k], s->pl_full[k]);
-    if (rc) return rc;
+    if ((rc = stencil(s->rl_full[k], s->pl_full[k], s->s_main))) return rc;
   } else {
-    HIP_TRY(hipEventRecord(s->ev_ready, s->s_main));
-    HIP_TRY(hipStreamWaitEvent(s->s_comm, s->ev_ready, 0));
-    if (launch_copy_lists(s->cl_pack[k], s->s_comm)) return NLH_ERR_HIP;
-    if (!s->peers.empty()) {
-      NCCL_TRY(ncclGroupStart());
-      for (auto &pr : s->peers) {
-        if (pr.send_count) NCCL_TRY(ncclSend(pr.send, pr.send_count, ncclDouble, pr.rank, s->comm, s->s_comm));
-        if (pr.recv_count) NCCL_TRY(ncclRecv(pr.recv, pr.recv_count, ncclDouble, pr.rank, s->comm, s->s_comm));
-      }
-      NCCL_TRY(ncclGroupEnd());
+    if (!s->halo_fresh) {  // first pass after test_init / set_field: this input's halo
+      HIP_TRY(hipEventRecord(s->ev_ready, s->s_main));
+      HIP_TRY(hipStreamWaitEvent(s->s_comm, s->ev_ready, 0));
+      if ((rc = enqueue_exchange(s, k))) return rc;
+      s->halo_fresh = true;
     }
-    if (launch_copy_lists(s->cl_unpack[k], s->s_comm)) return NLH_ERR_HIP;
-    if (launch_copy_lists(s->cl_local[k], s->s_comm)) return NLH_ERR_HIP;
-    HIP_TRY(hipEventRecord(s->ev_halo, s->s_comm));
-    int rc = stencil(s->rl_int[k], s->pl_int[k]);
-    if (rc) return rc;
-    HIP_TRY(hipStreamWaitEvent(s->s_main, s->ev_halo, 0));
-    rc = stencil(s->rl_bnd[k], s->pl_bnd[k]);
-    if (rc) return rc;
+    HIP_TRY(hipStreamWaitEvent(s->s_main, s->ev_band, 0));  // bands(n-1)
+    HIP_TRY(hipStreamWaitEvent(s->s_band, s->ev_int, 0));   // interior(n-1)
+    HIP_TRY(hipStreamWaitEvent(s->s_band, s->ev_halo, 0));  // halo(n)
+    if ((rc = stencil(s->rl_int[k], s->pl_int[k], s->s_main))) return rc;
+    HIP_TRY(hipEventRecord(s->ev_int, s->s_main));
+    if ((rc = stencil(s->rl_bnd[k], s->pl_bnd[k], s->s_band))) return rc;
+    HIP_TRY(hipEventRecord(s->ev_band, s->s_band));
+    HIP_TRY(hipStreamWaitEvent(s->s_comm, s->ev_band, 0));
+    if ((rc = enqueue_exchange(s, 1 - k))) return rc;
   }
   s->cur = 1 - k;
   s->t += nsteps;
@@ -439,6 +477,7 @@ int destroy_impl(nlh_solver *s) {
   (void)hipSetDevice(s->device);
   if (s->s_main) (void)hipStreamSynchronize(s->s_main);
   if (s->s_comm) (void)hipStreamSynchronize(s->s_comm);
+  if (s->s_band) (void)hipStreamSynchronize(s->s_band);
   if (s->comm) ncclCommDestroy(s->comm);
   for (auto &b : s->blocks) {
     (void)hipFree(b.base[0]);
@@ -457,8 +496,11 @@ int destroy_impl(nlh_solver *s) {
   for (auto e : s->ev_pool) (void)hipEventDestroy(e);
   if (s->ev_ready) (void)hipEventDestroy(s->ev_ready);
   if (s->ev_halo) (void)hipEventDestroy(s->ev_halo);
+  if (s->ev_band) (void)hipEventDestroy(s->ev_band);
+  if (s->ev_int) (void)hipEventDestroy(s->ev_int);
   if (s->s_main) (void)hipStreamDestroy(s->s_main);
   if (s->s_comm) (void)hipStreamDestroy(s->s_comm);
+  if (s->s_band) (void)hipStreamDestroy(s->s_band);
   delete s;
   return NLH_OK;
 }
@@ -523,6 +565,7 @@ int create_impl(const nlh_params *pin, nlh_solver *s) {
             std::isfinite(1.0 / alpha) && s->ablate == 0;
   if (const char *pe = std::getenv("NLH_PAIR")) s->pair = s->pair && std::atoi(pe) != 0;
   if (const char *pa = std::getenv("NLH_PAIR_ABLATE")) s->pair_ablate = std::atoi(pa);
+  if (const char *fb = std::getenv("NLH_FORCE_BANDS")) s->force_bands = std::atoi(fb) != 0;
   if (const char *ps = std::getenv("NLH_PAIR_SPLIT")) s->pair_split = std::min(2, std::max(0, std::atoi(ps)));
   if (s->pair_ablate >= 10000) s->pair_split = 1;
   s->halo = s->pair ? 2 * E : E;
@@ -530,8 +573,13 @@ int create_impl(const nlh_params *pin, nlh_solver *s) {
 
   HIP_TRY(hipStreamCreateWithFlags(&s->s_main, hipStreamNonBlocking));
   HIP_TRY(hipStreamCreateWithFlags(&s->s_comm, hipStreamNonBlocking));
+  HIP_TRY(hipStreamCreateWithFlags(&s->s_band, hipStreamNonBlocking));
   HIP_TRY(hipEventCreateWithFlags(&s->ev_ready, hipEventDisableTiming));
   HIP_TRY(hipEventCreateWithFlags(&s->ev_halo, hipEventDisableTiming));
+  HIP_TRY(hipEventCreateWithFlags(&s->ev_band, hipEventDisableTiming));
+  HIP_TRY(hipEventCreateWithFlags(&s->ev_int, hipEventDisableTiming));
+  HIP_TRY(hipEventRecord(s->ev_band, s->s_main));
+  HIP_TRY(hipEventRecord(s->ev_int, s->s_main));
 
   // ---- constants and host-computed tables (glibc sin, bit-equal to w())
   std::vector<double> sxt(p.nx + 2 * E), syt(p.ny + 2 * E);
@@ -577,10 +625,10 @@ int create_impl(const nlh_params *pin, nlh_solver *s) {
     const int64_t right = std::max(round_up(b.r.w, 256) + XL, s->pair ? b.r.w + 128 : 0);
     b.pitch = round_up(XL + right, 8) + pitch_pad;
     b.rows = b.r.h + 2 * s->halo;
-    b.L = b.r.x0 > 0;
-    b.Rr = b.r.x0 + b.r.w < p.nx;
-    b.T = b.r.y0 > 0;
-    b.B = b.r.y0 + b.r.h < p.ny;
+    b.L = b.r.x0 > 0 || s->force_bands;
+    b.Rr = b.r.x0 + b.r.w < p.nx || s->force_bands;
+    b.T = b.r.y0 > 0 || s->force_bands;
+    b.B = b.r.y0 + b.r.h < p.ny || s->force_bands;
     const size_t bytes = (size_t)(b.pitch * b.rows) * sizeof(double);
     for (int k = 0; k < 2; ++k) {
       HIP_TRY(hipMalloc(&b.base[k], bytes));
@@ -669,6 +717,7 @@ int nlh_init_test(nlh_solver *s) {
   HIP_TRY(hipStreamSynchronize(s->s_comm));
   s->cur = 0;
   s->t = 0;
+  s->halo_fresh = false;
   for (auto &b : s->blocks)
     if (nlh::launch_init_test(b.origin(0), b.pitch, (int)b.r.w, (int)b.r.h, (int)b.r.x0,
                               (int)b.r.y0, s->sc, s->s_main))
@@ -685,6 +734,7 @@ int nlh_set_field(nlh_solver *s, const double *u) {
   HIP_TRY(hipStreamSynchronize(s->s_main));
   s->cur = 0;
   s->t = 0;
+  s->halo_fresh = false;
   for (auto &b : s->blocks)
     HIP_TRY(hipMemcpy2D(b.origin(0), b.pitch * sizeof(double), u + b.r.y0 * s->p.nx + b.r.x0,
                         s->p.nx * sizeof(double), b.r.w * sizeof(double), b.r.h,
@@ -798,6 +848,7 @@ int nlh_run(nlh_solver *s, int64_t nsteps) {
       if ((rc = enqueue_step(s, 2))) return rc;
   for (; i < nsteps; ++i)
     if ((rc = enqueue_step(s, 1))) return rc;
+  if (s->exchange) HIP_TRY(hipStreamWaitEvent(s->s_main, s->ev_band, 0));  // last bands
   if (e1) {
     HIP_TRY(hipEventRecord(e1, s->s_main));
     s->ev_steps.push_back((int)nsteps);

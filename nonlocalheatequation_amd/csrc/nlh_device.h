@@ -26,9 +26,9 @@ struct Rect {
   int32_t gx0, gy0;   // global coordinates of node (0,0)
   int32_t x0, y0, x1, y1;
   int32_t wg_begin;   // first work item of this rect
-  int32_t nstrip;     // fast kernel: strips of 64*R columns
-  int32_t nseg;       // fast kernel: segments of seg_h rows
-  int32_t pad_;
+  int32_t nstrip;     // fast kernels: strips of output columns
+  int32_t nseg;       // fast kernels: segments of seg_rows rows
+  int32_t seg_rows;   // fast kernels: segment height of this rect
 };
 
 struct RectList {

@@ -65,7 +65,7 @@ __global__ __launch_bounds__(64) void k_fast(RectList L, StepConst C) {
   const int nstrip = Rc.nstrip;
   const int strip = local % nstrip, seg = local / nstrip;
   const int x0 = Rc.x0 + strip * W;
-  const int seg_h = C.seg_h;
+  const int seg_h = Rc.seg_rows;
   const int Y0 = Rc.y0 + seg * seg_h;
   const int Y1 = min(Y0 + seg_h, Rc.y1);
   const int n_in = (Y1 - Y0) + 2 * E;   // input rows Y0-E .. Y1+E-1

@@ -145,7 +145,7 @@ __global__ __launch_bounds__(64, (E <= 9 ? 2 : 1)) void k_pair(RectList L, StepC
   const int nstrip = Rc.nstrip;
   const int strip = local % nstrip, seg = local / nstrip;
   const int x0 = Rc.x0 + strip * WO;
-  const int seg_h = C.seg_pair;
+  const int seg_h = Rc.seg_rows;
   const int Y0 = Rc.y0 + seg * seg_h;
   const int Y1 = min(Y0 + seg_h, Rc.y1);
   const int n_in = (Y1 - Y0) + 4 * E;   // u^t rows Y0-2E .. Y1+2E-1
@@ -301,7 +301,7 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
   const int nstrip = Rc.nstrip;
   const int strip = local % nstrip, seg = local / nstrip;
   const int x0 = Rc.x0 + strip * WO;
-  const int seg_h = C.seg_pair;
+  const int seg_h = Rc.seg_rows;
   const int Y0 = Rc.y0 + seg * seg_h;
   const int Y1 = min(Y0 + seg_h, Rc.y1);
   const int n_in = (Y1 - Y0) + 4 * E;   // u^t rows Y0-2E .. Y1+2E-1
@@ -480,7 +480,7 @@ __global__ __launch_bounds__(192, 3) void k_pair_mw(RectList L, StepConst C) {
   const int nstrip = Rc.nstrip;
   const int strip = local % nstrip, seg = local / nstrip;
   const int x0 = Rc.x0 + strip * WO;
-  const int seg_h = C.seg_pair;
+  const int seg_h = Rc.seg_rows;
   const int Y0 = Rc.y0 + seg * seg_h;
   const int Y1 = min(Y0 + seg_h, Rc.y1);
   const int n_in = (Y1 - Y0) + 4 * E;

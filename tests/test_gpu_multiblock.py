@@ -128,3 +128,19 @@ def test_rccl_two_ranks_one_gpu(oracle):
     ref = oracle.run(oracle.params(nx, nx, 8, 1.0, dt, dh, 0), 5)
     u = res[0][1]
     assert np.max(np.abs(u - ref)) <= 1e-12 * np.max(np.abs(ref))
+
+
+@pytest.mark.parametrize("kernel,test", [("exact", True), ("fast", False), ("fast", True)])
+def test_forced_band_schedule_matches_oracle(oracle, monkeypatch, kernel, test):
+    """NLH_FORCE_BANDS runs one block through the multi-GPU schedule (interior
+    kernel, then the halo bands on their own stream with short segments)."""
+    monkeypatch.setenv("NLH_FORCE_BANDS", "1")
+    rng = np.random.default_rng(11)
+    nx, ny, eps, nt = 400, 300, 8, 5
+    u0 = rng.uniform(-1, 1, size=(ny, nx))
+    u, _, info, (k, dt, dh) = _run(nx, ny, eps, nt, test, kernel, (1, 1), False, u0=u0)
+    ref = oracle.run(oracle.params(nx, ny, eps, k, dt, dh, int(test)), nt, u0)
+    if kernel == "exact":
+        assert np.array_equal(u, ref)
+    else:
+        assert np.max(np.abs(u - ref)) <= 1e-12 * np.max(np.abs(ref))
