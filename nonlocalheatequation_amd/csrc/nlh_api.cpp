@@ -191,18 +191,32 @@ int build_rectlists(nlh_solver *s, int kind) {
     int64_t strip_rows = 0;
     for (auto &it : all) strip_rows += ceil_div(it.r.x1 - it.r.x0, sw) * (it.r.y1 - it.r.y0);
     const bool own = s->p.seg_rows > 0 && pair == s->pair;  // seg_rows tunes the kernel nlh_run uses most
-    if (pair) {  // one wave per workgroup, all resident at once: at most the
-                 // resident count, less one per strip column for the per-rect
-                 // rounding up of segments
-      int64_t strips = 0;
-      for (auto &it : all) strips += ceil_div(it.r.x1 - it.r.x0, sw);
+    if (pair) {
       // k_pair: every resident wave (2 per SIMD at E = 8); k_pair_split: 4
       // workgroups (8 waves) per CU -- taller segments beat more waves
-      // (profiles/r01/pair_v3)
+      // (profiles/r01/tune_v3b).  Segment height: minimise rounds x sweep,
+      // a sweep costing seg + 3E rows (stage 1 reads seg + 4E rows, stage 2
+      // seg + 2E); at 4096^2 this picks 152 rows = 999 workgroups in one
+      // round, the measured optimum; on large lattices several rounds of
+      // shorter segments instead of one round with idle slots
       const int per_cu = std::max(1, nlh::pair_blocks_per_cu(E, s->pair_split));
       const int64_t resident = (int64_t)(s->pair_split != 0 ? std::min(per_cu, 4) : per_cu) * s->cus;
-      const int64_t target = std::max<int64_t>(s->cus, resident - strips);
-      seg_h = own ? s->p.seg_rows : (int)std::max<int64_t>(16, ceil_div(strip_rows, target));
+      const std::vector<Item> &sized = inter.empty() ? all : inter;
+      int64_t hmax = 1;
+      for (auto &it : sized) hmax = std::max<int64_t>(hmax, it.r.y1 - it.r.y0);
+      int64_t best = -1, best_cost = 0;
+      for (int64_t n = 1; n <= 1024; ++n) {
+        const int64_t seg = std::max<int64_t>(16, ceil_div(hmax, n));
+        int64_t wgs = 0;
+        for (auto &it : sized) wgs += ceil_div(it.r.x1 - it.r.x0, sw) * ceil_div(it.r.y1 - it.r.y0, seg);
+        const int64_t cost = ceil_div(wgs, resident) * (seg + 3 * E);
+        if (best < 0 || cost < best_cost) {
+          best = seg;
+          best_cost = cost;
+        }
+        if (seg == 16) break;
+      }
+      seg_h = own ? s->p.seg_rows : (int)best;
     } else {
       seg_h = own ? s->p.seg_rows
                   : (int)std::max<int64_t>(nlh::fast_seg_min(E), ceil_div(strip_rows, 1024));
