@@ -95,6 +95,7 @@ struct nlh_solver {
   hipEvent_t ev_ready = nullptr, ev_halo = nullptr, ev_band = nullptr, ev_int = nullptr;
   bool halo_fresh = false;  // the current field's halo holds its neighbours' values
   bool force_bands = false;  // diagnostics (NLH_FORCE_BANDS): exchange-path schedule on one block
+  bool rccl_self = false;    // diagnostics (NLH_RCCL_SELF): one rank, local pieces over RCCL to self
   int64_t t = 0;
   int cur = 0;
   double *d_sxt = nullptr, *d_syt = nullptr;
@@ -302,11 +303,17 @@ int build_exchange(nlh_solver *s) {
   const int me = s->p.rank;
   std::map<int, size_t> local_of_plan;  // plan block index -> local index
   for (size_t i = 0; i < s->blocks.size(); ++i) local_of_plan[s->blocks[i].plan_index] = i;
+  // a piece travels over RCCL when its blocks sit on different ranks; with
+  // NLH_RCCL_SELF (diagnostics, one rank) every piece between two blocks of
+  // this rank goes through ncclSend/ncclRecv to self instead of a local copy,
+  // so the pack -> RCCL -> unpack path runs on a single GPU
+  auto remote = [&](const nlh::Piece &pc) { return pc.src_rank != pc.dst_rank || s->rccl_self; };
   // peers and message sizes in plan order
   std::map<int, Peer> peers;
   for (auto &pc : s->plan.pieces) {
-    if (pc.src_rank == me && pc.dst_rank != me) peers[pc.dst_rank].send_count += pc.r.w * pc.r.h;
-    if (pc.dst_rank == me && pc.src_rank != me) peers[pc.src_rank].recv_count += pc.r.w * pc.r.h;
+    if (!remote(pc)) continue;
+    if (pc.src_rank == me) peers[pc.dst_rank].send_count += pc.r.w * pc.r.h;
+    if (pc.dst_rank == me) peers[pc.src_rank].recv_count += pc.r.w * pc.r.h;
   }
   for (auto &kv : peers) {
     Peer &pr = kv.second;
@@ -325,18 +332,24 @@ int build_exchange(nlh_solver *s) {
     for (auto &pc : s->plan.pieces) {
       const int64_t n = pc.r.w * pc.r.h;
       int rc = NLH_OK;
-      if (pc.src_rank == me && pc.dst_rank == me) {
-        const LocalBlock &sb = s->blocks[local_of_plan[pc.src_block]];
-        const LocalBlock &db = s->blocks[local_of_plan[pc.dst_block]];
-        rc = add_copy(lc, node_ptr(sb, k, pc.r.x0, pc.r.y0), sb.pitch,
-                      node_ptr(db, k, pc.r.x0, pc.r.y0), db.pitch, pc.r.w, pc.r.h);
-      } else if (pc.src_rank == me) {
+      if (!remote(pc)) {
+        if (pc.src_rank == me) {
+          const LocalBlock &sb = s->blocks[local_of_plan[pc.src_block]];
+          const LocalBlock &db = s->blocks[local_of_plan[pc.dst_block]];
+          rc = add_copy(lc, node_ptr(sb, k, pc.r.x0, pc.r.y0), sb.pitch,
+                        node_ptr(db, k, pc.r.x0, pc.r.y0), db.pitch, pc.r.w, pc.r.h);
+        }
+        if (rc != NLH_OK) return rc;
+        continue;
+      }
+      if (pc.src_rank == me) {
         const LocalBlock &sb = s->blocks[local_of_plan[pc.src_block]];
         Peer &pr = peers[pc.dst_rank];
         rc = add_copy(pk, node_ptr(sb, k, pc.r.x0, pc.r.y0), sb.pitch,
                       pr.send + soff[pc.dst_rank], pc.r.w, pc.r.w, pc.r.h);
         soff[pc.dst_rank] += n;
-      } else if (pc.dst_rank == me) {
+      }
+      if (rc == NLH_OK && pc.dst_rank == me) {
         const LocalBlock &db = s->blocks[local_of_plan[pc.dst_block]];
         Peer &pr = peers[pc.src_rank];
         rc = add_copy(up, pr.recv + roff[pc.src_rank], pc.r.w,
@@ -580,6 +593,7 @@ int create_impl(const nlh_params *pin, nlh_solver *s) {
   if (const char *pe = std::getenv("NLH_PAIR")) s->pair = s->pair && std::atoi(pe) != 0;
   if (const char *pa = std::getenv("NLH_PAIR_ABLATE")) s->pair_ablate = std::atoi(pa);
   if (const char *fb = std::getenv("NLH_FORCE_BANDS")) s->force_bands = std::atoi(fb) != 0;
+  if (const char *rs = std::getenv("NLH_RCCL_SELF")) s->rccl_self = p.nranks == 1 && std::atoi(rs) != 0;
   if (const char *ps = std::getenv("NLH_PAIR_SPLIT")) s->pair_split = std::min(2, std::max(0, std::atoi(ps)));
   if (s->pair_ablate >= 10000) s->pair_split = 1;
   s->halo = s->pair ? 2 * E : E;
@@ -668,10 +682,14 @@ int create_impl(const nlh_params *pin, nlh_solver *s) {
     static_assert(sizeof(ncclUniqueId) == NLH_COMM_ID_BYTES, "unique id size");
     std::memcpy(&id, p.comm_id, sizeof(id));
     NCCL_TRY(ncclCommInitRank(&s->comm, p.nranks, id, p.rank));
+  } else if (s->rccl_self) {
+    ncclUniqueId id;
+    NCCL_TRY(ncclGetUniqueId(&id));
+    NCCL_TRY(ncclCommInitRank(&s->comm, 1, id, 0));
   }
   rc = build_exchange(s);
   if (rc) return rc;
-  if (s->exchange && p.nranks == 1 && !s->peers.empty())
+  if (s->exchange && !s->comm && !s->peers.empty())
     return fail(NLH_ERR_STATE, "internal: peers without communicator");
 
   // ---- norm scratch

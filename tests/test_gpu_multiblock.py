@@ -130,6 +130,27 @@ def test_rccl_two_ranks_one_gpu(oracle):
     assert np.max(np.abs(u - ref)) <= 1e-12 * np.max(np.abs(ref))
 
 
+@pytest.mark.parametrize("kernel,test,eps,nt", [("exact", True, 5, 6), ("fast", False, 8, 6),
+                                                ("fast", False, 8, 5), ("fast", True, 6, 4)])
+def test_rccl_self_transport(oracle, monkeypatch, kernel, test, eps, nt):
+    """NLH_RCCL_SELF: one rank with a size-1 RCCL communicator; every halo
+    piece between its blocks is packed, sent with ncclSend/ncclRecv to self
+    and unpacked -- the multi-GPU transport, on one MI355X."""
+    monkeypatch.setenv("NLH_RCCL_SELF", "1")
+    nx, ny, tiles = 384, 256, (3, 2)
+    rng = np.random.default_rng(5)
+    u0 = None if test else rng.uniform(-1, 1, size=(ny, nx))
+    u, (l2, li), info, (k, dt, dh) = _run(nx, ny, eps, nt, test, kernel, tiles, True, u0=u0)
+    assert info.nblocks == 6 and info.npeers == 1 and info.halo_bytes_sent > 0
+    p = oracle.params(nx, ny, eps, k, dt, dh, int(test))
+    ref = oracle.run(p, nt, u0)
+    if kernel == "exact":
+        assert np.array_equal(u, ref)
+        assert li == oracle.errors(p, nt, ref)[1]
+    else:
+        assert np.max(np.abs(u - ref)) <= 1e-12 * np.max(np.abs(ref))
+
+
 @pytest.mark.parametrize("kernel,test", [("exact", True), ("fast", False), ("fast", True)])
 def test_forced_band_schedule_matches_oracle(oracle, monkeypatch, kernel, test):
     """NLH_FORCE_BANDS runs one block through the multi-GPU schedule (interior
