@@ -46,24 +46,34 @@ def decomposition(n: int):
     return px, n // px
 
 
-def cpu_baseline(nthreads: int, budget_s: float = 12.0) -> dict:
+def cpu_baseline(nthreads: int, nb: int = NB, eps: int = EPS, test: bool = False,
+                 budget_s: float = 12.0) -> dict:
     """Oracle restatement of 2d_nonlocal_async (np x np tiles, one task per
-    tile per step, a barrier per step) on the same 4096^2 / eps=8 workload,
+    tile per step, a barrier per step) on the same nb^2 / eps workload,
     bounded to ~budget_s of CPU time."""
     from oracle import oracle as O  # test infrastructure: baseline leg only
 
-    dh = 1.0 / NB
-    dt = EPS ** 4 * dh * dh / (8.0 * N.disk_count(EPS))
-    p = O.params(NB, NB, EPS, 1.0, dt, dh, 0)
+    dh = 1.0 / nb
+    dt = eps ** 4 * dh * dh / (8.0 * N.disk_count(eps))
+    p = O.params(nb, nb, eps, 1.0, dt, dh, int(test))
     u = O.test_init(p)
-    tiles = 32  # 128 x 128-node tiles
+    tiles = max(1, nb // 128)  # 128 x 128-node tiles
     t1 = O.run_tiled(p, 1, tiles, tiles, u, nthreads)
     steps = int(max(1, min(20, budget_s / max(t1, 1e-3) - 1)))
     t = O.run_tiled(p, steps, tiles, tiles, u, nthreads)
-    rate = NB * NB * steps / t / 1e9
+    rate = nb * nb * steps / t / 1e9
     return {"value": rate, "unit": "Gnode-updates/s", "cores": nthreads, "kind": "port",
-            "sample": f"{NB}x{NB} lattice, eps={EPS}, test=0, {steps} step(s) after 1 warm-up step, "
+            "sample": f"{nb}x{nb} lattice, eps={eps}, test={int(test)}, {steps} step(s) after 1 warm-up step, "
                       f"{tiles}x{tiles} tiles, oracle/nlh_oracle.c run_tiled (-O3 -ffp-contract=off)"}
+
+
+def workload_name(nb, eps, strong, test, nx, ny) -> str:
+    mode = "test mode (manufactured source)" if test else "production step (test=0)"
+    if not strong and nb == NB and eps == EPS:
+        return f"C2: {nb}x{nb} lattice per GPU, eps={eps}, {mode}"
+    if strong:
+        return f"{nx}x{ny} lattice in total (strong scaling), eps={eps}, {mode}"
+    return f"{nb}x{nb} lattice per GPU, eps={eps}, {mode}"
 
 
 def read_traffic(kernel_name: str):
@@ -89,7 +99,15 @@ def main() -> int:
     ap.add_argument("--kernel", default="fast", choices=["fast", "exact"])
     ap.add_argument("--seg-rows", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    # secondary workloads (the default line is C2): --eps 32 --lattice 8192 is
+    # C4; --lattice 32768 --strong is C3 (total lattice fixed as N grows);
+    # --test-mode times the manufactured-solution step and reports its L2
+    ap.add_argument("--eps", type=int, default=EPS)
+    ap.add_argument("--lattice", type=int, default=NB, help="lattice edge per GPU (weak) or total (--strong)")
+    ap.add_argument("--strong", action="store_true")
+    ap.add_argument("--test-mode", action="store_true")
     args = ap.parse_args()
+    eps, nb = args.eps, args.lattice
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -104,9 +122,15 @@ def main() -> int:
         dist.init_process_group("gloo")
 
     px, py = decomposition(nranks)
-    nx, ny = NB * px, NB * py
-    dh = 1.0 / NB
-    dt = EPS ** 4 * dh * dh / (8.0 * N.disk_count(EPS))
+    if args.strong:
+        if nb % px or nb % py:
+            print(f"--lattice {nb} is not divisible by the {px}x{py} block grid", file=sys.stderr)
+            return 2
+        nx, ny = nb, nb
+    else:
+        nx, ny = nb * px, nb * py
+    dh = 1.0 / nb
+    dt = eps ** 4 * dh * dh / (8.0 * N.disk_count(eps))
 
     comm_id = None
     if nranks > 1:
@@ -114,7 +138,7 @@ def main() -> int:
         dist.broadcast_object_list(obj, src=0)
         comm_id = obj[0]
 
-    s = N.Solver(nx, ny, EPS, 1.0, dt, dh, test=False, kernel=args.kernel, device=local,
+    s = N.Solver(nx, ny, eps, 1.0, dt, dh, test=args.test_mode, kernel=args.kernel, device=local,
                  rank=rank, nranks=nranks, tiles=(px, py), comm_id=comm_id, seg_rows=args.seg_rows)
     s.test_init()
     s.run(args.warmup)
@@ -143,6 +167,7 @@ def main() -> int:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    l2 = s.compute_l2(s.step_index) if args.test_mode else None  # after the timed region
     info = s.info()
     total_nodes = nx * ny
     value = total_nodes * args.steps / elapsed / 1e9
@@ -155,18 +180,23 @@ def main() -> int:
     passes = max(k_n // spp, 1)
     avg_launch_s = (k_ms / 1e3) / passes
     # algorithmic bytes per launch = 16 B per node-update x node-updates of one launch
-    alg_bytes = BYTES_PER_NODE * local_nodes * spp
+    # + 8 B per node when the fast test mode reads its precomputed L_h[W0]
+    bytes_node = BYTES_PER_NODE + (8.0 if args.test_mode and info.kernel == N.KERNEL_FAST else 0.0)
+    alg_bytes = bytes_node * local_nodes * spp
     achieved_gbs = alg_bytes / avg_launch_s / 1e9
     fp64_equiv_tflops = 2.0 * info.disk_points * local_nodes * spp / avg_launch_s / 1e12
-    traffic = read_traffic(kname) if nranks == 1 else None
+    # the committed PMC summary was taken on the default C2 workload only
+    default_wl = nb == NB and eps == EPS and not args.strong and not args.test_mode
+    traffic = read_traffic(kname) if nranks == 1 and default_wl else None
 
     result = None
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and nranks == 1:
-            cpu = cpu_baseline(nthreads=min(16, os.cpu_count() or 1))
+            # bounded sample: at most a 4096^2 lattice of the same eps / mode
+            cpu = cpu_baseline(min(16, os.cpu_count() or 1), min(nb, NB), eps, args.test_mode)
         result = {
-            "metric": "Gnode-updates/s (nodes*steps/s) eps=8 fp64",
+            "metric": f"Gnode-updates/s (nodes*steps/s) eps={eps} fp64",
             "value": value,
             "unit": "Gnode-updates/s",
             "n_gpus": nranks,
@@ -174,14 +204,14 @@ def main() -> int:
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.strong else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (test_init IC sin(2 pi x) sin(2 pi y); no dataset)",
             "config": {
-                "workload": f"C2: {NB}x{NB} lattice per GPU, eps={EPS}, production step (test=0), "
-                            f"{args.kernel} kernel" + (f", {px}x{py} blocks + RCCL ghost exchange" if nranks > 1 else ""),
-                "lattice": [nx, ny], "eps": EPS, "blocks": [px, py],
+                "workload": workload_name(nb, eps, args.strong, args.test_mode, nx, ny)
+                            + f", {args.kernel} kernel" + (f", {px}x{py} blocks + RCCL ghost exchange" if nranks > 1 else ""),
+                "lattice": [nx, ny], "eps": eps, "blocks": [px, py], "test_mode": args.test_mode,
                 "disk_points": info.disk_points, "dt": dt, "dh": dh, "kernel": args.kernel,
             },
             "roofline": {
@@ -201,6 +231,8 @@ def main() -> int:
             },
             "cpu_baseline": cpu,
         }
+        if l2 is not None:
+            result["config"]["l2_error"] = l2  # reference error_l2 at the final step
         print(json.dumps(result), flush=True)
     s.close()
     if dist is not None:

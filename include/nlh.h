@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define NLH_ABI_VERSION 3
+#define NLH_ABI_VERSION 4
 
 enum nlh_status {
   NLH_OK = 0,
@@ -107,6 +107,19 @@ int nlh_get_field(nlh_solver *s, double *u_global);
 int nlh_gather_field(nlh_solver *s, int32_t root, double *u_global);
 /* Collective: returns once every rank has finished its enqueued steps.    */
 int nlh_barrier(nlh_solver *s);
+
+/* Asynchronous snapshot of this rank's owned nodes for logging, replacing
+ * the synchronous S[next] reads of the reference's log steps
+ * (src/2d_nonlocal_serial.cpp:286-290, 149-177; async :214-284).
+ * nlh_snapshot_begin enqueues, behind the steps enqueued so far, a device
+ * copy of the current field and its transfer into library-owned pinned host
+ * memory on a copy stream, and returns at once: later nlh_run calls overlap
+ * the transfer.  nlh_snapshot_wait blocks until that snapshot landed and
+ * scatters it into u_global (x + y*nx, owned nodes only); it may be called
+ * from another host thread than the one enqueueing steps.  One snapshot in
+ * flight at a time (NLH_ERR_STATE otherwise).                             */
+int nlh_snapshot_begin(nlh_solver *s);
+int nlh_snapshot_wait(nlh_solver *s, double *u_global);
 
 /* Advance `nsteps` explicit-Euler steps from the current step index.
  * Asynchronous: returns once the work is enqueued (nlh_synchronize waits). */

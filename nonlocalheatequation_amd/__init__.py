@@ -81,6 +81,8 @@ _SIGNATURES = {
     "nlh_run": ([ctypes.c_void_p, ctypes.c_int64], ctypes.c_int),
     "nlh_gather_field": ([ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
     "nlh_barrier": ([ctypes.c_void_p], ctypes.c_int),
+    "nlh_snapshot_begin": ([ctypes.c_void_p], ctypes.c_int),
+    "nlh_snapshot_wait": ([ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
     "nlh_synchronize": ([ctypes.c_void_p], ctypes.c_int),
     "nlh_step_index": ([ctypes.c_void_p], ctypes.c_int64),
     "nlh_errors": ([ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_double),
@@ -314,6 +316,18 @@ class Solver:
         """Collective: the global field on rank `root` (None elsewhere)."""
         out = np.zeros((self.ny, self.nx), dtype=np.float64)
         _check(lib().nlh_gather_field(self._h, int(root), _dp(out)), "nlh_gather_field")
+        return out
+
+    def snapshot_begin(self) -> None:
+        """Enqueue an asynchronous copy of the owned nodes (logging path)."""
+        _check(lib().nlh_snapshot_begin(self._h), "nlh_snapshot_begin")
+
+    def snapshot_wait(self, out: np.ndarray | None = None) -> np.ndarray:
+        """The snapshot of the last snapshot_begin(), owned nodes in a global
+        (ny, nx) array."""
+        if out is None:
+            out = np.zeros((self.ny, self.nx), dtype=np.float64)
+        _check(lib().nlh_snapshot_wait(self._h, _dp(out)), "nlh_snapshot_wait")
         return out
 
     def barrier(self) -> None:

@@ -121,7 +121,7 @@ int main(int argc, char **argv) {
       lg.nx = b.nx * b.npx, lg.ny = b.ny * b.npy, lg.dt = b.dt, lg.dh = b.dh, lg.test = true;
       lg.probe();
       uint64_t el = 0;
-      if (run_steps(s, b.nt, nlog, lg, true, re.rank, el) != NLH_OK) return die("nlh_run");
+      if (run_steps(s, b.nt, nlog, lg, true, re.rank, el, re.nranks) != NLH_OK) return die("nlh_run");
       double l2 = 0, linf = 0;
       if (nlh_errors(s, b.nt, &l2, &linf) != NLH_OK) return die("nlh_errors");
       nlh_destroy(s);
@@ -149,7 +149,7 @@ int main(int argc, char **argv) {
   lg.nx = gx, lg.ny = gy, lg.dt = r.dt, lg.dh = r.dh, lg.test = r.test;
   lg.probe();
   uint64_t elapsed = 0;
-  if (run_steps(s, r.nt, nlog, lg, true, re.rank, elapsed) != NLH_OK) return die("nlh_run");
+  if (run_steps(s, r.nt, nlog, lg, true, re.rank, elapsed, re.nranks) != NLH_OK) return die("nlh_run");
 
   if (o.count("test_load_balance") && re.rank == 0)
     std::cerr << "[note] static block decomposition: no dynamic load balancing to test" << std::endl;

@@ -280,10 +280,20 @@ void Logger::log(int64_t t, int64_t vtk_index, const std::vector<double> &u) {
 
 // ---------------------------------------------------------------- loop
 int run_steps(nlh_solver *s, int64_t nt, int64_t nlog, Logger &lg, bool vtk_index_is_t,
-              int rank, uint64_t &elapsed_ns) {
+              int rank, uint64_t &elapsed_ns, int nranks) {
   const bool logging = lg.enabled() && nlog > 0;
+  // one rank: log steps take an asynchronous snapshot (device copy in stream
+  // order, host transfer on a copy stream) and a writer thread formats the
+  // files while the next steps run; several ranks gather to rank 0 (RCCL)
+  const bool async_log = logging && nranks == 1;
   std::vector<double> u;
   if (logging) u.assign((size_t)(lg.nx * lg.ny), 0.0);
+  std::thread writer;
+  int wrc = NLH_OK;  // writer status (read after join)
+  auto join_writer = [&]() -> int {
+    if (writer.joinable()) writer.join();
+    return wrc;
+  };
   int rc = nlh_barrier(s);
   if (rc) return rc;
   const uint64_t t0 = now_ns();
@@ -294,13 +304,26 @@ int run_steps(nlh_solver *s, int64_t nt, int64_t nlog, Logger &lg, bool vtk_inde
       const int64_t next_log = (t % nlog == 0) ? t : (t / nlog + 1) * nlog;
       last = std::min(last, next_log);
     }
-    if ((rc = nlh_run(s, last - t + 1)) != NLH_OK) return rc;
+    if ((rc = nlh_run(s, last - t + 1)) != NLH_OK) break;
     t = last + 1;
     if (logging && last % nlog == 0) {
-      if ((rc = nlh_gather_field(s, 0, rank == 0 ? u.data() : nullptr)) != NLH_OK) return rc;
-      if (rank == 0) lg.log(last, vtk_index_is_t ? last : last / nlog, u);
+      const int64_t vi = vtk_index_is_t ? last : last / nlog;
+      if (async_log) {
+        if ((rc = join_writer()) != NLH_OK) break;  // one snapshot in flight
+        if ((rc = nlh_snapshot_begin(s)) != NLH_OK) break;
+        writer = std::thread([&, last, vi] {
+          wrc = nlh_snapshot_wait(s, u.data());
+          if (wrc == NLH_OK) lg.log(last, vi, u);
+        });
+      } else {
+        if ((rc = nlh_gather_field(s, 0, rank == 0 ? u.data() : nullptr)) != NLH_OK) break;
+        if (rank == 0) lg.log(last, vi, u);
+      }
     }
   }
+  const int jr = join_writer();
+  if (rc == NLH_OK) rc = jr;
+  if (rc != NLH_OK) return rc;
   if ((rc = nlh_barrier(s)) != NLH_OK) return rc;
   elapsed_ns = now_ns() - t0;
   return NLH_OK;

@@ -85,10 +85,13 @@ void print_errors(double l2, double linf);
 // The reference's do_work time loop with its logging cadence: after step t,
 // if t % nlog == 0, log S[next] (serial names the VTK file t/nlog, the tiled
 // solvers t).  Steps between log points are enqueued back to back.  Collective
-// when nranks > 1 (the field is gathered to rank 0 for logging).  Returns
-// NLH_OK and the wall time of the loop (all ranks finished) in elapsed_ns.
+// when nranks > 1 (the field is gathered to rank 0 for logging); with one
+// rank the log steps snapshot the field asynchronously (nlh_snapshot_begin)
+// and a writer thread writes the files while the following steps run.
+// Returns NLH_OK and the wall time of the loop (all ranks finished, the last
+// files written) in elapsed_ns.
 int run_steps(nlh_solver *s, int64_t nt, int64_t nlog, Logger &lg, bool vtk_index_is_t,
-              int rank, uint64_t &elapsed_ns);
+              int rank, uint64_t &elapsed_ns, int nranks = 1);
 
 // Read the reference's --file partition file (src/2d_nonlocal_distributed.cpp:
 // 467-488): "nx ny npx npy dh" then npx*npy lines "px py owner", px outer.

@@ -18,6 +18,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -96,6 +97,14 @@ struct nlh_solver {
   bool halo_fresh = false;  // the current field's halo holds its neighbours' values
   bool force_bands = false;  // diagnostics (NLH_FORCE_BANDS): exchange-path schedule on one block
   bool rccl_self = false;    // diagnostics (NLH_RCCL_SELF): one rank, local pieces over RCCL to self
+  bool exchange_planned = false;  // the plan has halo pieces (set before the rect lists)
+  // exchange schedule (profiles/r01/sched): interior workgroups per CU in the
+  // segment model when an exchange runs beside it (RCCL kernels need the LDS
+  // a fourth k_pair_split workgroup would hold; NLH_INT_PER_CU, 0 = all), and
+  // where the bands run (NLH_SCHED): 2 = on the exchange stream (default),
+  // 0 = own stream beside the interior, 1 = before the interior on s_main
+  int int_per_cu = 3;
+  int sched = 2;
   int64_t t = 0;
   int cur = 0;
   double *d_sxt = nullptr, *d_syt = nullptr;
@@ -123,6 +132,12 @@ struct nlh_solver {
   std::vector<int> ev_steps;  // time steps covered by each timed event pair
   int64_t device_bytes = 0;
   char arch[32] = {0};
+  // logging snapshots (nlh_snapshot_begin / _wait): owned nodes packed block
+  // after block, device copy then pinned host copy on s_copy
+  hipStream_t s_copy = nullptr;
+  hipEvent_t ev_snap_dev = nullptr, ev_snap = nullptr;
+  double *snap_dev = nullptr, *snap_host = nullptr;
+  std::atomic<bool> snap_pending{false};
 };
 
 namespace {
@@ -201,7 +216,16 @@ int build_rectlists(nlh_solver *s, int kind) {
       // round, the measured optimum; on large lattices several rounds of
       // shorter segments instead of one round with idle slots
       const int per_cu = std::max(1, nlh::pair_blocks_per_cu(E, s->pair_split));
-      const int64_t resident = (int64_t)(s->pair_split != 0 ? std::min(per_cu, 4) : per_cu) * s->cus;
+      int use_cu = s->pair_split != 0 ? std::min(per_cu, 4) : per_cu;
+      // with an exchange the interior may be sized for fewer slots per CU,
+      // leaving room for the bands and RCCL beside it (NLH_INT_PER_CU)
+      // -- measured a win up to 4096^2-sized blocks (166 vs 182 us/step for
+      // four 4096^2 blocks over RCCL), a loss on the 16384 x 8192 share of C3
+      int64_t big = 0;
+      for (auto &b : s->blocks) big = std::max<int64_t>(big, b.r.w * b.r.h);
+      if (s->exchange_planned && s->int_per_cu > 0 && big <= (int64_t)4096 * 8192)
+        use_cu = std::min(use_cu, s->int_per_cu);
+      const int64_t resident = (int64_t)use_cu * s->cus;
       const std::vector<Item> &sized = inter.empty() ? all : inter;
       int64_t hmax = 1;
       for (auto &it : sized) hmax = std::max<int64_t>(hmax, it.r.y1 - it.r.y0);
@@ -457,13 +481,37 @@ int enqueue_step(nlh_solver *s, int nsteps) {
       if ((rc = enqueue_exchange(s, k))) return rc;
       s->halo_fresh = true;
     }
-    HIP_TRY(hipStreamWaitEvent(s->s_main, s->ev_band, 0));  // bands(n-1)
-    HIP_TRY(hipStreamWaitEvent(s->s_band, s->ev_int, 0));   // interior(n-1)
-    HIP_TRY(hipStreamWaitEvent(s->s_band, s->ev_halo, 0));  // halo(n)
-    if ((rc = stencil(s->rl_int[k], s->pl_int[k], s->s_main))) return rc;
-    HIP_TRY(hipEventRecord(s->ev_int, s->s_main));
-    if ((rc = stencil(s->rl_bnd[k], s->pl_bnd[k], s->s_band))) return rc;
-    HIP_TRY(hipEventRecord(s->ev_band, s->s_band));
+    if (s->sched == 1) {
+      // bands(n) then interior(n), both on s_main: the bands run alone
+      // briefly and the interior keeps its one-round grid
+      HIP_TRY(hipStreamWaitEvent(s->s_main, s->ev_halo, 0));  // halo(n)
+      if ((rc = stencil(s->rl_bnd[k], s->pl_bnd[k], s->s_main))) return rc;
+      HIP_TRY(hipEventRecord(s->ev_band, s->s_main));
+      if ((rc = stencil(s->rl_int[k], s->pl_int[k], s->s_main))) return rc;
+    } else if (s->sched == 2) {
+      // bands(n) on the exchange stream, right before the exchange they feed:
+      // the chain bands -> pack -> send/recv -> unpack -> next bands crosses
+      // no queue; only interior(n-1) -> bands(n) and bands(n-1) -> interior(n)
+      // do (about 11 us per cross-queue wait, profiles/r01/sched)
+      HIP_TRY(hipStreamWaitEvent(s->s_main, s->ev_band, 0));  // bands(n-1)
+      HIP_TRY(hipStreamWaitEvent(s->s_comm, s->ev_int, 0));   // interior(n-1)
+      if ((rc = stencil(s->rl_int[k], s->pl_int[k], s->s_main))) return rc;
+      HIP_TRY(hipEventRecord(s->ev_int, s->s_main));
+      if ((rc = stencil(s->rl_bnd[k], s->pl_bnd[k], s->s_comm))) return rc;
+      HIP_TRY(hipEventRecord(s->ev_band, s->s_comm));
+      if ((rc = enqueue_exchange(s, 1 - k))) return rc;
+      s->cur = 1 - k;
+      s->t += nsteps;
+      return NLH_OK;
+    } else {
+      HIP_TRY(hipStreamWaitEvent(s->s_main, s->ev_band, 0));  // bands(n-1)
+      HIP_TRY(hipStreamWaitEvent(s->s_band, s->ev_int, 0));   // interior(n-1)
+      HIP_TRY(hipStreamWaitEvent(s->s_band, s->ev_halo, 0));  // halo(n)
+      if ((rc = stencil(s->rl_int[k], s->pl_int[k], s->s_main))) return rc;
+      HIP_TRY(hipEventRecord(s->ev_int, s->s_main));
+      if ((rc = stencil(s->rl_bnd[k], s->pl_bnd[k], s->s_band))) return rc;
+      HIP_TRY(hipEventRecord(s->ev_band, s->s_band));
+    }
     HIP_TRY(hipStreamWaitEvent(s->s_comm, s->ev_band, 0));
     if ((rc = enqueue_exchange(s, 1 - k))) return rc;
   }
@@ -505,7 +553,13 @@ int destroy_impl(nlh_solver *s) {
   if (s->s_main) (void)hipStreamSynchronize(s->s_main);
   if (s->s_comm) (void)hipStreamSynchronize(s->s_comm);
   if (s->s_band) (void)hipStreamSynchronize(s->s_band);
+  if (s->s_copy) (void)hipStreamSynchronize(s->s_copy);
   if (s->comm) ncclCommDestroy(s->comm);
+  (void)hipFree(s->snap_dev);
+  if (s->snap_host) (void)hipHostFree(s->snap_host);
+  if (s->ev_snap_dev) (void)hipEventDestroy(s->ev_snap_dev);
+  if (s->ev_snap) (void)hipEventDestroy(s->ev_snap);
+  if (s->s_copy) (void)hipStreamDestroy(s->s_copy);
   for (auto &b : s->blocks) {
     (void)hipFree(b.base[0]);
     (void)hipFree(b.base[1]);
@@ -594,14 +648,19 @@ int create_impl(const nlh_params *pin, nlh_solver *s) {
   if (const char *pa = std::getenv("NLH_PAIR_ABLATE")) s->pair_ablate = std::atoi(pa);
   if (const char *fb = std::getenv("NLH_FORCE_BANDS")) s->force_bands = std::atoi(fb) != 0;
   if (const char *rs = std::getenv("NLH_RCCL_SELF")) s->rccl_self = p.nranks == 1 && std::atoi(rs) != 0;
+  if (const char *ic = std::getenv("NLH_INT_PER_CU")) s->int_per_cu = std::max(0, std::atoi(ic));
+  if (const char *sc = std::getenv("NLH_SCHED")) s->sched = std::min(2, std::max(0, std::atoi(sc)));
+  int prio_lo = 0, prio_hi = 0;  // NLH_COMM_PRIO=1: exchange + band streams at the highest priority
+  if (const char *cp = std::getenv("NLH_COMM_PRIO"))
+    if (std::atoi(cp) != 0) HIP_TRY(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
   if (const char *ps = std::getenv("NLH_PAIR_SPLIT")) s->pair_split = std::min(2, std::max(0, std::atoi(ps)));
   if (s->pair_ablate >= 10000) s->pair_split = 1;
   s->halo = s->pair ? 2 * E : E;
   s->plan = nlh::make_plan(p.nx, p.ny, s->halo, tx, ty, s->owner, p.split_tiles == 0);
 
   HIP_TRY(hipStreamCreateWithFlags(&s->s_main, hipStreamNonBlocking));
-  HIP_TRY(hipStreamCreateWithFlags(&s->s_comm, hipStreamNonBlocking));
-  HIP_TRY(hipStreamCreateWithFlags(&s->s_band, hipStreamNonBlocking));
+  HIP_TRY(hipStreamCreateWithPriority(&s->s_comm, hipStreamNonBlocking, prio_hi));
+  HIP_TRY(hipStreamCreateWithPriority(&s->s_band, hipStreamNonBlocking, prio_hi));
   HIP_TRY(hipEventCreateWithFlags(&s->ev_ready, hipEventDisableTiming));
   HIP_TRY(hipEventCreateWithFlags(&s->ev_halo, hipEventDisableTiming));
   HIP_TRY(hipEventCreateWithFlags(&s->ev_band, hipEventDisableTiming));
@@ -671,6 +730,7 @@ int create_impl(const nlh_params *pin, nlh_solver *s) {
     s->blocks.push_back(b);
   }
 
+  s->exchange_planned = !s->plan.pieces.empty() || s->force_bands;
   int rc = build_rectlists(s, 0);
   if (rc) return rc;
   if (s->pair && (rc = build_rectlists(s, 1))) return rc;
@@ -856,6 +916,55 @@ int nlh_barrier(nlh_solver *s) {
     NCCL_TRY(ncclAllReduce(s->d_red, s->d_red, 1, ncclDouble, ncclSum, s->comm, s->s_comm));
     HIP_TRY(hipStreamSynchronize(s->s_comm));
   }
+  return NLH_OK;
+}
+
+int nlh_snapshot_begin(nlh_solver *s) {
+  if (!s) return fail(NLH_ERR_ARG, "null solver");
+  if (s->snap_pending) return fail(NLH_ERR_STATE, "a snapshot is already in flight (call nlh_snapshot_wait)");
+  int rc = set_device(s);
+  if (rc) return rc;
+  int64_t owned = 0;
+  for (auto &b : s->blocks) owned += b.r.w * b.r.h;
+  if (!s->snap_dev) {  // first snapshot: buffers and the copy stream
+    HIP_TRY(hipMalloc(&s->snap_dev, std::max<int64_t>(owned, 1) * sizeof(double)));
+    HIP_TRY(hipHostMalloc(&s->snap_host, std::max<int64_t>(owned, 1) * sizeof(double), hipHostMallocDefault));
+    HIP_TRY(hipStreamCreateWithFlags(&s->s_copy, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&s->ev_snap_dev, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&s->ev_snap, hipEventDisableTiming));
+    s->device_bytes += owned * (int64_t)sizeof(double);
+  }
+  // the device copy sits on the step stream behind every enqueued pass (its
+  // last bands included, nlh_run ends s_main on them), so the next pass cannot
+  // overwrite the parity buffer before it is read; the slow host transfer then
+  // runs on s_copy beside the following passes
+  int64_t off = 0;
+  for (auto &b : s->blocks) {
+    HIP_TRY(hipMemcpy2DAsync(s->snap_dev + off, b.r.w * sizeof(double), b.origin(s->cur),
+                             b.pitch * sizeof(double), b.r.w * sizeof(double), b.r.h,
+                             hipMemcpyDeviceToDevice, s->s_main));
+    off += b.r.w * b.r.h;
+  }
+  HIP_TRY(hipEventRecord(s->ev_snap_dev, s->s_main));
+  HIP_TRY(hipStreamWaitEvent(s->s_copy, s->ev_snap_dev, 0));
+  HIP_TRY(hipMemcpyAsync(s->snap_host, s->snap_dev, std::max<int64_t>(owned, 1) * sizeof(double),
+                         hipMemcpyDeviceToHost, s->s_copy));
+  HIP_TRY(hipEventRecord(s->ev_snap, s->s_copy));
+  s->snap_pending = true;
+  return NLH_OK;
+}
+
+int nlh_snapshot_wait(nlh_solver *s, double *u) {
+  if (!s || !u) return fail(NLH_ERR_ARG, "null argument");
+  if (!s->snap_pending) return fail(NLH_ERR_STATE, "no snapshot in flight");
+  HIP_TRY(hipEventSynchronize(s->ev_snap));
+  int64_t off = 0;
+  for (auto &b : s->blocks) {
+    for (int64_t y = 0; y < b.r.h; ++y)
+      std::memcpy(u + (b.r.y0 + y) * s->p.nx + b.r.x0, s->snap_host + off + y * b.r.w, b.r.w * sizeof(double));
+    off += b.r.w * b.r.h;
+  }
+  s->snap_pending = false;
   return NLH_OK;
 }
 

@@ -165,3 +165,29 @@ def test_forced_band_schedule_matches_oracle(oracle, monkeypatch, kernel, test):
         assert np.array_equal(u, ref)
     else:
         assert np.max(np.abs(u - ref)) <= 1e-12 * np.max(np.abs(ref))
+
+
+@pytest.mark.parametrize("tiles,split,kernel", [((1, 1), False, "exact"), ((3, 2), True, "exact"),
+                                                ((2, 2), True, "fast")])
+def test_snapshot_overlaps_later_steps(oracle, tiles, split, kernel):
+    """nlh_snapshot_begin after step n, more steps enqueued behind it, then
+    nlh_snapshot_wait: the snapshot is u(n), the field u(n + m)."""
+    nx, ny, eps, n, m = 192, 128, 6, 5, 4
+    dh = 1.0 / nx
+    dt = eps ** 4 * dh * dh / (8 * N.disk_count(eps))
+    p = oracle.params(nx, ny, eps, 1.0, dt, dh, 1)
+    with N.Solver(nx, ny, eps, 1.0, dt, dh, test=True, kernel=kernel, tiles=tiles, split_tiles=split) as s:
+        s.test_init()
+        s.run(n)
+        s.snapshot_begin()
+        with pytest.raises(N.NLHError):
+            s.snapshot_begin()  # one snapshot in flight
+        s.run(m)
+        snap = s.snapshot_wait()
+        u = s.field()
+    for got, t in ((snap, n), (u, n + m)):
+        ref = oracle.run(p, t)
+        if kernel == "exact":
+            assert np.array_equal(got, ref)
+        else:
+            assert np.max(np.abs(got - ref)) <= 1e-12 * np.max(np.abs(ref))
