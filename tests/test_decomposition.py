@@ -121,6 +121,8 @@ CASES = [
     dict(name="eps > tile, split tiles", nx=30, ny=20, eps=7, nt=2, tiles=(6, 4), owner=None, split=True, world=3),
     dict(name="25s_8n map folded to 3 ranks", nx=50, ny=50, eps=4, nt=3, tiles=(5, 5), owner="25s_8n",
          split=False, world=3),
+    # bench.py --gpus 8 layout (decomposition(8) = 4x2 blocks, one per rank, locidx owners)
+    dict(name="bench N=8 layout 4x2", nx=64, ny=32, eps=6, nt=3, tiles=(4, 2), owner=None, split=False, world=8),
 ]
 
 
