@@ -7,50 +7,79 @@ Workload (BASELINE.json configs[1]): a 4096 x 4096
 lattice PER GPU, eps = 8, fp64, production mode (test=0: the nonlocal
 operator only, as in the reference's non-test runs), synthetic test_init IC,
 k = 1, dh = 1/4096, dt = eps^4 dh^2 / (8 k N(eps)).  One "step" = one explicit
-Euler step of the whole lattice.  N > 1 GPUs: one process per GPU (launched by
-torch.distributed.run), the lattice grows with N (weak scaling) as a px x py
-block decomposition with eps-wide ghost strips exchanged over RCCL each step.
+Euler step of the whole lattice.
+
+N > 1 GPUs: one process per GPU.  Under torch.distributed.run (RANK /
+WORLD_SIZE set) every process is one rank; with WORLD_SIZE unset,
+``--gpus N`` starts the N rank processes itself (before any GPU call) and
+rank 0 prints the line.  Weak scaling by default: the lattice grows with N as
+a px x py block decomposition (1x1, 2x1, 2x2, 2x4 -- the C4/C5 layouts),
+ghost strips exchanged over RCCL.  ``--strong --lattice 32768`` fixes the
+total lattice (C3: 2x4 blocks of 16384 x 8192 on 8 GPUs).
 
 Prints one JSON line (rank 0) with the roofline of the dominant kernel
-(HIP events on the stencil's own stream) and a bounded CPU baseline (the
-oracle's tiled 2d_nonlocal_async restatement on the host cores).
+(HIP events on the stencil's own stream), its physical limits from the
+committed rocprofv3 PMC profile of the same kernel and workload, and a
+bounded CPU baseline (the oracle's tiled 2d_nonlocal_async restatement on
+the host cores this job may use).
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
-import numpy as np
-
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-
-import nonlocalheatequation_amd as N  # noqa: E402
 
 EPS = 8
 NB = 4096                      # lattice per GPU (each direction)
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 FP64_VEC_PEAK_TFLOPS = 78.6    # 256 CU x 64 lanes x 2 x 2.4 GHz (spec)
+FP64_LANE_OPS_PEAK = 256 * 64 * 2.4e9  # f64 VALU lane-operations per second (spec clock)
 BYTES_PER_NODE = 16.0          # read u once + write u' once (SURVEY 8(d))
 
 
 def decomposition(n: int):
+    """px x py blocks for n ranks: 1x1, 2x1, 2x2, 2x4,
+    else px the largest power of two with px^2 <= n dividing n."""
+    if n == 2:
+        return 2, 1
     px = 1
-    while px * px < n:
+    while (2 * px) * (2 * px) <= n and n % (2 * px) == 0:
         px *= 2
-    while n % px:
-        px //= 2
     return px, n // px
 
 
+def host_cpu_share() -> int:
+    """Host threads this job may use: the CPU affinity mask, capped by the
+    cgroup CPU quota and by OMP_NUM_THREADS when the launcher sets it (the GPU
+    box exports its per-GPU CPU share there; nproc shows the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, math.ceil(int(quota) / int(period))))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
 def cpu_baseline(nthreads: int, nb: int = NB, eps: int = EPS, test: bool = False,
-                 budget_s: float = 12.0) -> dict:
+                 budget_s: float = 15.0) -> dict:
     """Oracle restatement of 2d_nonlocal_async (np x np tiles, one task per
     tile per step, a barrier per step) on the same nb^2 / eps workload,
-    bounded to ~budget_s of CPU time."""
+    bounded to ~budget_s of wall time."""
+    import nonlocalheatequation_amd as N
     from oracle import oracle as O  # test infrastructure: baseline leg only
 
     dh = 1.0 / nb
@@ -59,12 +88,18 @@ def cpu_baseline(nthreads: int, nb: int = NB, eps: int = EPS, test: bool = False
     u = O.test_init(p)
     tiles = max(1, nb // 128)  # 128 x 128-node tiles
     t1 = O.run_tiled(p, 1, tiles, tiles, u, nthreads)
-    steps = int(max(1, min(20, budget_s / max(t1, 1e-3) - 1)))
+    steps = int(max(1, min(200, budget_s / max(t1, 1e-3) - 1)))
     t = O.run_tiled(p, steps, tiles, tiles, u, nthreads)
     rate = nb * nb * steps / t / 1e9
     return {"value": rate, "unit": "Gnode-updates/s", "cores": nthreads, "kind": "port",
-            "sample": f"{nb}x{nb} lattice, eps={eps}, test={int(test)}, {steps} step(s) after 1 warm-up step, "
-                      f"{tiles}x{tiles} tiles, oracle/nlh_oracle.c run_tiled (-O3 -ffp-contract=off)"}
+            "host_cpus_visible": os.cpu_count(),
+            "sample": f"{nb}x{nb} lattice, eps={eps}, test={int(test)}, {steps} step(s) after 1 warm-up step "
+                      f"({t:.1f} s), {tiles}x{tiles} tiles on {nthreads} threads (the job's host CPU share), "
+                      f"oracle/nlh_oracle.c run_tiled (-O3 -ffp-contract=off)"}
+
+
+def workload_key(nb, eps, strong, test) -> str:
+    return f"{'strong' if strong else 'weak'}_{nb}_eps{eps}_{'test' if test else 'prod'}"
 
 
 def workload_name(nb, eps, strong, test, nx, ny) -> str:
@@ -76,19 +111,58 @@ def workload_name(nb, eps, strong, test, nx, ny) -> str:
     return f"{nb}x{nb} lattice per GPU, eps={eps}, {mode}"
 
 
-def read_traffic(kernel_name: str):
-    """HBM bytes per stencil launch from the committed rocprofv3 PMC summary
-    (FETCH_SIZE doubled per the gfx950 correction + WRITE_SIZE), if that
-    summary was taken on the kernel this run launches."""
-    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+def read_pmc(kernel_name: str, wkey: str):
+    """The committed rocprofv3 PMC summary of this kernel on this workload
+    (tools/pmc_summary.py: FETCH_SIZE doubled per the gfx950 correction +
+    WRITE_SIZE, SQ_INSTS_VALU; separate passes), if one exists."""
+    path = os.path.join(ROOT, "profiles", "pmc", f"{kernel_name}__{wkey}.json")
     try:
         with open(path) as f:
             d = json.load(f)
     except (OSError, ValueError):
-        return None
-    if d.get("kernel_match") != kernel_name:
-        return None
-    return d.get("hbm_bytes_per_launch")
+        return None, path
+    if d.get("kernel_match") != kernel_name or d.get("workload") != wkey:
+        return None, path
+    return d, path
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn_ranks(n: int) -> int:
+    """Start n rank processes of this script (RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_* in their environment) and wait for them.  The parent never
+    touches the GPU."""
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ)
+        env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    # a rank that fails would leave the others blocked in a collective: stop
+    # them (these exact child processes) as soon as one exits non-zero
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            r = p.poll()
+            if r is None:
+                continue
+            live.remove(p)
+            if r != 0:
+                rc = max(rc, abs(r))
+                for q in live:
+                    q.terminate()
+        time.sleep(0.2)
+    return rc
 
 
 def main() -> int:
@@ -96,7 +170,7 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=50)
-    ap.add_argument("--kernel", default="fast", choices=["fast", "exact"])
+    ap.add_argument("--kernel", default="fast", choices=["fast", "exact", "auto"])
     ap.add_argument("--seg-rows", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     # secondary workloads (the default line is C2): --eps 32 --lattice 8192 is
@@ -109,17 +183,26 @@ def main() -> int:
     args = ap.parse_args()
     eps, nb = args.eps, args.lattice
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return spawn_ranks(args.gpus)
+
+    import nonlocalheatequation_amd as N
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.gpus != world and world > 1:
+    if args.gpus != world:
         print(f"--gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+        return 2
     nranks = world
 
     dist = None
     if nranks > 1:
         import torch.distributed as dist  # control plane only (id broadcast, barrier, max)
         dist.init_process_group("gloo")
+        if dist.get_world_size() != args.gpus:
+            print(f"process group has {dist.get_world_size()} ranks, expected {args.gpus}", file=sys.stderr)
+            return 3
 
     px, py = decomposition(nranks)
     if args.strong:
@@ -140,6 +223,17 @@ def main() -> int:
 
     s = N.Solver(nx, ny, eps, 1.0, dt, dh, test=args.test_mode, kernel=args.kernel, device=local,
                  rank=rank, nranks=nranks, tiles=(px, py), comm_id=comm_id, seg_rows=args.seg_rows)
+    info = s.info()
+    # every rank owns exactly one block of the px x py grid: the communicator
+    # and the plan both see all N ranks
+    owned = [info.owned_nodes]
+    if dist is not None:
+        lst = [None] * nranks
+        dist.all_gather_object(lst, (info.owned_nodes, info.nblocks))
+        owned = [o for o, _ in lst]
+        if sum(owned) != nx * ny or any(o == 0 for o in owned):
+            print(f"ranks own {owned} nodes of {nx * ny}", file=sys.stderr)
+            return 3
     s.test_init()
     s.run(args.warmup)
     s.synchronize()
@@ -168,13 +262,12 @@ def main() -> int:
         elapsed = float(t.item())
 
     l2 = s.compute_l2(s.step_index) if args.test_mode else None  # after the timed region
-    info = s.info()
     total_nodes = nx * ny
     value = total_nodes * args.steps / elapsed / 1e9
     ms_per_step = elapsed * 1e3 / args.steps
     local_nodes = info.owned_nodes
     # one stencil launch (a "pass") advances steps_per_pass time steps: 2 for
-    # the temporally blocked production kernel k_pair, 1 for k_fast / k_exact
+    # the temporally blocked production kernel k_pair_split, 1 for k_fast / k_exact
     spp = info.steps_per_pass
     kname = info.pass_kernel
     passes = max(k_n // spp, 1)
@@ -182,24 +275,51 @@ def main() -> int:
     # algorithmic bytes per launch = 16 B per node-update x node-updates of one launch
     # + 8 B per node when the fast test mode reads its precomputed L_h[W0]
     bytes_node = BYTES_PER_NODE + (8.0 if args.test_mode and info.kernel == N.KERNEL_FAST else 0.0)
-    alg_bytes = bytes_node * local_nodes * spp
+    nu_launch = local_nodes * spp
+    alg_bytes = bytes_node * nu_launch
     achieved_gbs = alg_bytes / avg_launch_s / 1e9
-    fp64_equiv_tflops = 2.0 * info.disk_points * local_nodes * spp / avg_launch_s / 1e12
-    # the committed PMC summary was taken on the default C2 workload only
-    default_wl = nb == NB and eps == EPS and not args.strong and not args.test_mode
-    traffic = read_traffic(kname) if nranks == 1 and default_wl else None
+    fp64_equiv_tflops = 2.0 * info.disk_points * nu_launch / avg_launch_s / 1e12
+
+    wkey = workload_key(nb, eps, args.strong, args.test_mode)
+    pmc, pmc_path = read_pmc(kname, wkey) if nranks == 1 else (None, None)
+    traffic = pmc["hbm_bytes_per_launch"] if pmc else None
+    physical = None
+    if pmc:
+        # what the kernel actually moves and issues (PMC), and the ceiling
+        # those counts allow: min(HBM spec / bytes, f64 VALU issue / lane-ops)
+        b_nu = pmc["hbm_bytes_per_launch"] / pmc["node_updates_per_launch"]
+        ops_nu = pmc["valu_insts_per_launch"] * 64.0 / pmc["node_updates_per_launch"]
+        hbm_ceiling = HBM_PEAK_GBS * 1e9 / b_nu / 1e9
+        valu_ceiling = FP64_LANE_OPS_PEAK / ops_nu / 1e9
+        rate_launch = nu_launch / avg_launch_s / 1e9  # G node-updates/s of the kernel alone
+        physical = {
+            "hbm_bytes_per_node_update": b_nu,
+            "hbm_frac": pmc["hbm_bytes_per_launch"] / avg_launch_s / 1e9 / HBM_PEAK_GBS,
+            "valu_lane_ops_per_node_update": ops_nu,
+            "valu_frac": pmc["valu_insts_per_launch"] * 64.0 / avg_launch_s / FP64_LANE_OPS_PEAK,
+            "hbm_ceiling_gnu": hbm_ceiling,
+            "valu_ceiling_gnu": valu_ceiling,
+            "ceiling_gnu": min(hbm_ceiling, valu_ceiling),
+            "limiter": "hbm" if hbm_ceiling < valu_ceiling else "fp64_valu_issue",
+            "kernel_rate_gnu": rate_launch,
+            "frac_of_ceiling": rate_launch / min(hbm_ceiling, valu_ceiling),
+            "wait_share_of_wave_cycles": pmc.get("share_of_wave_cycles", {}).get("SQ_WAIT_ANY"),
+            "source": os.path.relpath(pmc_path, ROOT),
+            "profiled_commit": pmc.get("commit"),
+        }
 
     result = None
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and nranks == 1:
             # bounded sample: at most a 4096^2 lattice of the same eps / mode
-            cpu = cpu_baseline(min(16, os.cpu_count() or 1), min(nb, NB), eps, args.test_mode)
+            cpu = cpu_baseline(host_cpu_share(), min(nb, NB), eps, args.test_mode)
         result = {
             "metric": f"Gnode-updates/s (nodes*steps/s) eps={eps} fp64",
             "value": value,
             "unit": "Gnode-updates/s",
             "n_gpus": nranks,
+            "nranks_seen": len(owned),
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
@@ -213,21 +333,29 @@ def main() -> int:
                             + f", {args.kernel} kernel" + (f", {px}x{py} blocks + RCCL ghost exchange" if nranks > 1 else ""),
                 "lattice": [nx, ny], "eps": eps, "blocks": [px, py], "test_mode": args.test_mode,
                 "disk_points": info.disk_points, "dt": dt, "dh": dh, "kernel": args.kernel,
+                "parallelism": f"{px}x{py} block decomposition, one rank per GPU" if nranks > 1 else "1 GPU",
             },
             "roofline": {
+                # contract: achieved = ALGORITHMIC bytes (16 B per
+                # node-update) per launch / average launch duration.  The two-step
+                # pass moves ~0.56x those bytes, so frac is an effective
+                # bandwidth; the physical limits are in roofline.physical
                 "bound": "hbm",
                 "achieved": achieved_gbs,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved_gbs / HBM_PEAK_GBS,
                 "traffic": traffic,
+                "achieved_is": "effective (algorithmic bytes / launch time)",
                 "kernel": kname,
                 "steps_per_launch": spp,
                 "kernel_avg_us": avg_launch_s * 1e6,
                 "kernel_launches_timed": passes,
                 "algorithmic_bytes_per_launch": alg_bytes,
+                "node_updates_per_launch": nu_launch,
                 "fp64_direct_sum_equiv_tflops": fp64_equiv_tflops,
                 "fp64_direct_sum_equiv_frac": fp64_equiv_tflops / FP64_VEC_PEAK_TFLOPS,
+                "physical": physical,
             },
             "cpu_baseline": cpu,
         }

@@ -55,10 +55,11 @@ enum nlh_status {
 
 /* Stencil implementation.  EXACT reproduces the reference's per-term
  * floating-point order bit for bit (4 ops per neighbour).  FAST computes the
- * same J=1 disk sum by nested row windows (~4*eps adds per node, HBM-bound);
- * it differs from the reference only by summation rounding.  AUTO = EXACT
- * when the manufactured source is on (test=1, where the L2 error is the
- * output), FAST otherwise (production runs).                             */
+ * same J=1 disk sum by nested row windows (~4*eps adds per node) and, in test
+ * mode, the manufactured source from a precomputed L_h[W0] field; it differs
+ * from the reference only by summation rounding (<= 1e-12 of field scale per
+ * node, L2 error within 1e-10).  AUTO = FAST wherever it is instantiated
+ * (production and test mode), EXACT otherwise.                            */
 enum nlh_kernel { NLH_KERNEL_AUTO = 0, NLH_KERNEL_EXACT = 1, NLH_KERNEL_FAST = 2 };
 
 typedef struct nlh_params {
@@ -165,7 +166,9 @@ int nlh_resolve_owner(int64_t tiles_x, int64_t tiles_y, int32_t nranks,
                       const int32_t *owner_in, int32_t *owner_out);
 
 /* Host-only halo plan, for tests of the decomposition: number of halo
- * pieces this rank receives per step and, if `pieces` is non-NULL, up to
+ * pieces this rank receives per pass (halo width: the one nlh_create resolves
+ * for the same parameters -- 2*eps when production fast mode runs two steps
+ * per pass, eps otherwise) and, if `pieces` is non-NULL, up to
  * `cap` records of 8 int64 each:
  *   {src_rank, dst_rank, gx0, gy0, w, h, src_block, dst_block}
  * (a global rectangle copied from the owner's interior into the halo of

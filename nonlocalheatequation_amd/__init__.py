@@ -168,10 +168,11 @@ def _make_params(nx, ny, eps, k, dt, dh, test, kernel, device, rank, nranks, seg
     return p, keep
 
 
-def block_plan(nx, ny, eps, tiles=(1, 1), owner=None, nranks=1, split_tiles=False) -> np.ndarray:
+def block_plan(nx, ny, eps, tiles=(1, 1), owner=None, nranks=1, split_tiles=False, *,
+               k=1.0, dt=1.0, dh=1.0, test=False, kernel="auto") -> np.ndarray:
     """Host-only block plan over all ranks: (n, 6) int64 rows
     {rank, local_index, gx0, gy0, w, h}."""
-    p, keep = _make_params(nx, ny, eps, 1.0, 1.0, 1.0, 0, KERNEL_AUTO, -1, 0, nranks, 0,
+    p, keep = _make_params(nx, ny, eps, k, dt, dh, test, kernel, -1, 0, nranks, 0,
                            tiles, owner, None, split_tiles)
     n = lib().nlh_block_plan(ctypes.byref(p), None, 0)
     if n < 0:
@@ -183,10 +184,15 @@ def block_plan(nx, ny, eps, tiles=(1, 1), owner=None, nranks=1, split_tiles=Fals
     return out
 
 
-def halo_plan(nx, ny, eps, tiles=(1, 1), owner=None, rank=0, nranks=1, split_tiles=False) -> np.ndarray:
+def halo_plan(nx, ny, eps, tiles=(1, 1), owner=None, rank=0, nranks=1, split_tiles=False, *,
+              k=1.0, dt=1.0, dh=1.0, test=False, kernel="auto") -> np.ndarray:
     """Host-only halo plan: (n, 8) int64 rows
-    {src_rank, dst_rank, gx0, gy0, w, h, src_block, dst_block} received by `rank`."""
-    p, keep = _make_params(nx, ny, eps, 1.0, 1.0, 1.0, 0, KERNEL_AUTO, -1, rank, nranks, 0,
+    {src_rank, dst_rank, gx0, gy0, w, h, src_block, dst_block} received by `rank`.
+
+    The halo width is the one nlh_create resolves for the same parameters:
+    2*eps when production fast mode runs the two-step pass (test=False,
+    kernel auto/fast, eps with a pair instantiation), eps otherwise."""
+    p, keep = _make_params(nx, ny, eps, k, dt, dh, test, kernel, -1, rank, nranks, 0,
                            tiles, owner, None, split_tiles)
     n = lib().nlh_halo_plan(ctypes.byref(p), None, 0)
     if n < 0:
@@ -266,7 +272,13 @@ class Solver:
 
     # -- reference interface ---------------------------------------------
     def test_init(self) -> None:
-        self.test = True
+        """u(0) = sin(2 pi x dh) sin(2 pi y dh) (test_init, :190-198).
+
+        The reference's test_init() also switches the manufactured source on
+        (test = 1).  Here the source is fixed when the solver is created
+        (``test=``), so ``test_init()`` only sets the IC: with ``test=False`` it
+        is the production run from the sine IC (the benchmark's workload) and
+        ``do_work`` computes no error norms."""
         _check(lib().nlh_init_test(self._h), "nlh_init_test")
 
     def input_init(self, u: np.ndarray) -> None:

@@ -90,11 +90,17 @@ int main(int argc, char **argv) {
   const int device = (int)o.as_i64("device");
   const int64_t nlog = (int64_t)o.as_u64("nlog");
 
+  // RCCL unique ids are single-use (the bootstrap root serves one
+  // communicator): rank 0 makes a fresh one for every solver, batch rows
+  // included, and serves it over the TCP bootstrap
   uint8_t id[NLH_COMM_ID_BYTES] = {0};
-  if (re.nranks > 1 && !share_comm_id(re, id, err)) {
-    std::cerr << err << std::endl;
-    return 1;
-  }
+  auto fresh_id = [&]() {
+    if (re.nranks > 1 && !share_comm_id(re, id, err)) {
+      std::cerr << err << std::endl;
+      return false;
+    }
+    return true;
+  };
 
   Run r{};
   r.nx = o.as_i64("nx");
@@ -116,6 +122,7 @@ int main(int argc, char **argv) {
       std::cin >> b.nx >> b.ny >> b.npx >> b.npy >> b.nt >> b.eps >> b.k >> b.dt >> b.dh;
       b.test = true;
       nlh_solver *s = nullptr;
+      if (!fresh_id()) return 1;
       if (make_solver(b, re, id, kernel, device, &s)) return 1;
       Logger lg;
       lg.nx = b.nx * b.npx, lg.ny = b.ny * b.npy, lg.dt = b.dt, lg.dh = b.dh, lg.test = true;
@@ -143,6 +150,7 @@ int main(int argc, char **argv) {
   if (file != "None") read_partition_file(file, r.nx, r.ny, r.npx, r.npy, r.dh, r.owner);
 
   nlh_solver *s = nullptr;
+  if (!fresh_id()) return 1;
   if (make_solver(r, re, id, kernel, device, &s)) return 1;
   const int64_t gx = r.nx * r.npx, gy = r.ny * r.npy;
   Logger lg;

@@ -57,6 +57,51 @@ int fail(int code, const std::string &msg) {
 int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
 int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// Stencil kernel, steps per pass and halo width for a parameter set: one
+// resolution shared by nlh_create and the host-only plan queries, so the
+// plans tests inspect are the ones production builds.
+struct Resolved {
+  int kernel = NLH_KERNEL_EXACT;
+  bool pair = false;  // two steps per pass (nlh_pair.h)
+  int halo = 0;       // eps, or 2*eps with pair
+  int ablate = 0;     // diagnostics only (NLH_ABLATE)
+};
+
+int resolve_config(const nlh_params &p, Resolved &r) {
+  const int E = (int)p.eps;
+  int kern = p.kernel;
+  // AUTO: the fast kernels in production AND test mode (the manufactured
+  // source in its precomputed L_h[W0] form, within 1e-12 of field scale and
+  // L2 within 1e-10 of the reference; EXACT remains selectable for bitwise
+  // parity)
+  if (kern == NLH_KERNEL_AUTO) kern = NLH_KERNEL_FAST;
+  if (kern == NLH_KERNEL_FAST && !nlh::fast_supported(E)) {
+    if (p.kernel == NLH_KERNEL_FAST)
+      return fail(NLH_ERR_UNSUPPORTED, "fast kernel not instantiated for eps=" + std::to_string(E));
+    kern = NLH_KERNEL_EXACT;
+  }
+  r.kernel = kern;
+  r.ablate = 0;
+  if (const char *ab = std::getenv("NLH_ABLATE")) r.ablate = std::atoi(ab);
+  // production fast mode advances two steps per pass; the source term of the
+  // test mode and a zero alpha (no centre fold) keep the single-step kernels
+  const double alpha = ((p.k * 8) / pow(p.eps * p.dh, 4)) * (p.dh * p.dh) * p.dt;
+  r.pair = kern == NLH_KERNEL_FAST && !p.test && nlh::pair_supported(E) && alpha != 0.0 &&
+           std::isfinite(1.0 / alpha) && r.ablate == 0;
+  if (const char *pe = std::getenv("NLH_PAIR")) r.pair = r.pair && std::atoi(pe) != 0;
+  r.halo = r.pair ? 2 * E : E;
+  return NLH_OK;
+}
+
+// NLH_VIRTUAL_RANKS=V (diagnostics, one rank): resolve the owner map over V
+// virtual owners; every block stays on this GPU
+int virtual_ranks(const nlh_params &p) {
+  if (p.nranks != 1) return 0;
+  const char *v = std::getenv("NLH_VIRTUAL_RANKS");
+  const int n = v ? std::atoi(v) : 0;
+  return n > 1 ? n : 0;
+}
+
 struct LocalBlock {
   int plan_index = 0;
   nlh::GRect r;
@@ -98,6 +143,9 @@ struct nlh_solver {
   bool force_bands = false;  // diagnostics (NLH_FORCE_BANDS): exchange-path schedule on one block
   bool rccl_self = false;    // diagnostics (NLH_RCCL_SELF): one rank, local pieces over RCCL to self
   bool exchange_planned = false;  // the plan has halo pieces (set before the rect lists)
+  // NLH_VIRTUAL_RANKS: per plan piece, 1 if it crosses virtual owners (goes
+  // over RCCL to self); empty otherwise
+  std::vector<uint8_t> vremote;
   // exchange schedule (profiles/r01/sched): interior workgroups per CU in the
   // segment model when an exchange runs beside it (RCCL kernels need the LDS
   // a fourth k_pair_split workgroup would hold; NLH_INT_PER_CU, 0 = all), and
@@ -330,12 +378,20 @@ int build_exchange(nlh_solver *s) {
   // a piece travels over RCCL when its blocks sit on different ranks; with
   // NLH_RCCL_SELF (diagnostics, one rank) every piece between two blocks of
   // this rank goes through ncclSend/ncclRecv to self instead of a local copy,
-  // so the pack -> RCCL -> unpack path runs on a single GPU
-  auto remote = [&](const nlh::Piece &pc) { return pc.src_rank != pc.dst_rank || s->rccl_self; };
+  // so the pack -> RCCL -> unpack path runs on a single GPU.  With
+  // NLH_VIRTUAL_RANKS (diagnostics) only pieces between blocks of different
+  // virtual owners do: the block structure and message pattern of a
+  // multi-rank run, every rank's blocks on this one GPU.
+  auto remote = [&](size_t pi) {
+    const nlh::Piece &pc = s->plan.pieces[pi];
+    if (!s->vremote.empty()) return s->vremote[pi] != 0;
+    return pc.src_rank != pc.dst_rank || s->rccl_self;
+  };
   // peers and message sizes in plan order
   std::map<int, Peer> peers;
-  for (auto &pc : s->plan.pieces) {
-    if (!remote(pc)) continue;
+  for (size_t pi = 0; pi < s->plan.pieces.size(); ++pi) {
+    const nlh::Piece &pc = s->plan.pieces[pi];
+    if (!remote(pi)) continue;
     if (pc.src_rank == me) peers[pc.dst_rank].send_count += pc.r.w * pc.r.h;
     if (pc.dst_rank == me) peers[pc.src_rank].recv_count += pc.r.w * pc.r.h;
   }
@@ -353,10 +409,11 @@ int build_exchange(nlh_solver *s) {
     pk.clear();
     up.clear();
     lc.clear();
-    for (auto &pc : s->plan.pieces) {
+    for (size_t pi = 0; pi < s->plan.pieces.size(); ++pi) {
+      const nlh::Piece &pc = s->plan.pieces[pi];
       const int64_t n = pc.r.w * pc.r.h;
       int rc = NLH_OK;
-      if (!remote(pc)) {
+      if (!remote(pi)) {
         if (pc.src_rank == me) {
           const LocalBlock &sb = s->blocks[local_of_plan[pc.src_block]];
           const LocalBlock &db = s->blocks[local_of_plan[pc.dst_block]];
@@ -603,7 +660,9 @@ int create_impl(const nlh_params *pin, nlh_solver *s) {
   s->p.comm_id = nullptr;
 
   std::string err;
-  if (!nlh::resolve_owner(tx, ty, p.nranks, p.owner, s->owner, err)) return fail(NLH_ERR_ARG, err);
+  const int vranks = virtual_ranks(p);
+  if (!nlh::resolve_owner(tx, ty, vranks ? vranks : p.nranks, p.owner, s->owner, err))
+    return fail(NLH_ERR_ARG, err);
 
   // ---- device
   int ndev = 0;
@@ -625,29 +684,21 @@ int create_impl(const nlh_params *pin, nlh_solver *s) {
 
   // ---- kernel choice
   const int E = (int)p.eps;
-  int kern = p.kernel;
-  if (kern == NLH_KERNEL_AUTO) kern = p.test ? NLH_KERNEL_EXACT : NLH_KERNEL_FAST;
-  if (kern == NLH_KERNEL_FAST && !nlh::fast_supported(E)) {
-    if (p.kernel == NLH_KERNEL_FAST)
-      return fail(NLH_ERR_UNSUPPORTED, "fast kernel not instantiated for eps=" + std::to_string(E));
-    kern = NLH_KERNEL_EXACT;
-  }
+  Resolved rv;
+  if (int rc0 = resolve_config(p, rv)) return rc0;
+  const int kern = rv.kernel;
   s->kernel = kern;
   if (const char *r = std::getenv("NLH_FAST_R")) {
     const int v = std::atoi(r);
     s->fast_r = (v == 1 || v == 4) ? v : 2;
   }
   s->fast_r = nlh::fast_lanes_cols(E, s->fast_r);
-  if (const char *ab = std::getenv("NLH_ABLATE")) s->ablate = std::atoi(ab);
-  // production fast mode advances two steps per pass; the source term of the
-  // test mode and a zero alpha (no centre fold) keep the single-step kernels
-  const double alpha = ((p.k * 8) / pow(p.eps * p.dh, 4)) * (p.dh * p.dh) * p.dt;
-  s->pair = kern == NLH_KERNEL_FAST && !p.test && nlh::pair_supported(E) && alpha != 0.0 &&
-            std::isfinite(1.0 / alpha) && s->ablate == 0;
-  if (const char *pe = std::getenv("NLH_PAIR")) s->pair = s->pair && std::atoi(pe) != 0;
+  s->ablate = rv.ablate;
+  s->pair = rv.pair;
   if (const char *pa = std::getenv("NLH_PAIR_ABLATE")) s->pair_ablate = std::atoi(pa);
   if (const char *fb = std::getenv("NLH_FORCE_BANDS")) s->force_bands = std::atoi(fb) != 0;
   if (const char *rs = std::getenv("NLH_RCCL_SELF")) s->rccl_self = p.nranks == 1 && std::atoi(rs) != 0;
+  if (vranks) s->rccl_self = true;  // virtual owners talk over RCCL to self
   if (const char *ic = std::getenv("NLH_INT_PER_CU")) s->int_per_cu = std::max(0, std::atoi(ic));
   if (const char *sc = std::getenv("NLH_SCHED")) s->sched = std::min(2, std::max(0, std::atoi(sc)));
   int prio_lo = 0, prio_hi = 0;  // NLH_COMM_PRIO=1: exchange + band streams at the highest priority
@@ -655,8 +706,18 @@ int create_impl(const nlh_params *pin, nlh_solver *s) {
     if (std::atoi(cp) != 0) HIP_TRY(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
   if (const char *ps = std::getenv("NLH_PAIR_SPLIT")) s->pair_split = std::min(2, std::max(0, std::atoi(ps)));
   if (s->pair_ablate >= 10000) s->pair_split = 1;
-  s->halo = s->pair ? 2 * E : E;
+  s->halo = rv.halo;
   s->plan = nlh::make_plan(p.nx, p.ny, s->halo, tx, ty, s->owner, p.split_tiles == 0);
+  if (vranks) {
+    // blocks keep the virtual owners' shapes; all of them live on rank 0
+    s->vremote.resize(s->plan.pieces.size());
+    for (size_t i = 0; i < s->plan.pieces.size(); ++i) {
+      nlh::Piece &pc = s->plan.pieces[i];
+      s->vremote[i] = pc.src_rank != pc.dst_rank;
+      pc.src_rank = pc.dst_rank = 0;
+    }
+    for (auto &b : s->plan.blocks) b.rank = 0;
+  }
 
   HIP_TRY(hipStreamCreateWithFlags(&s->s_main, hipStreamNonBlocking));
   HIP_TRY(hipStreamCreateWithPriority(&s->s_comm, hipStreamNonBlocking, prio_hi));
@@ -1117,7 +1178,11 @@ int64_t nlh_halo_plan(const nlh_params *p, int64_t *pieces, int64_t cap) {
   std::vector<int32_t> o;
   std::string err;
   if (!nlh::resolve_owner(tx, ty, p->nranks, p->owner, o, err)) return -fail(NLH_ERR_ARG, err);
-  nlh::Plan plan = nlh::make_plan(p->nx, p->ny, p->eps, tx, ty, o, p->split_tiles == 0);
+  // the halo width production resolves for these parameters (eps, or 2*eps
+  // for the two-step pass)
+  Resolved rv;
+  if (int rc = resolve_config(*p, rv)) return -rc;
+  nlh::Plan plan = nlh::make_plan(p->nx, p->ny, rv.halo, tx, ty, o, p->split_tiles == 0);
   int64_t n = 0;
   for (auto &pc : plan.pieces) {
     if (pc.dst_rank != p->rank) continue;
@@ -1145,7 +1210,11 @@ int64_t nlh_block_plan(const nlh_params *p, int64_t *blocks, int64_t cap) {
   std::vector<int32_t> o;
   std::string err;
   if (!nlh::resolve_owner(tx, ty, p->nranks, p->owner, o, err)) return -fail(NLH_ERR_ARG, err);
-  nlh::Plan plan = nlh::make_plan(p->nx, p->ny, p->eps, tx, ty, o, p->split_tiles == 0);
+  // the halo width production resolves for these parameters (eps, or 2*eps
+  // for the two-step pass)
+  Resolved rv;
+  if (int rc = resolve_config(*p, rv)) return -rc;
+  nlh::Plan plan = nlh::make_plan(p->nx, p->ny, rv.halo, tx, ty, o, p->split_tiles == 0);
   int64_t n = 0;
   for (auto &b : plan.blocks) {
     if (blocks && n < cap) {

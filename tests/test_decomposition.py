@@ -38,15 +38,17 @@ def _lens(eps):
     return [int(np.floor(np.sqrt(float(eps * eps - d * d)))) for d in range(eps + 1)]
 
 
-def block_step(P, E, w, h, c2d, dh2, dt, lens):
-    """sum_local (src/2d_nonlocal_serial.cpp:256-270) on a padded block, same
-    per-term order: sx outer, sy inner, res += ((c*(u_j-u_i))*dh^2)."""
-    u = P[E:E + h, E:E + w]
+def block_step(P, H, x0, y0, x1, y1, c2d, dh2, dt, lens, E):
+    """sum_local (src/2d_nonlocal_serial.cpp:256-270) on the block-local
+    rectangle [x0, x1) x [y0, y1) of a block padded by H, same per-term order:
+    sx outer, sy inner, res += ((c*(u_j-u_i))*dh^2).  Needs H >= E beyond the
+    rectangle."""
+    u = P[H + y0:H + y1, H + x0:H + x1]
     res = np.zeros_like(u)
     for dx in range(-E, E + 1):
         ln = lens[abs(dx)]
         for dy in range(-ln, ln + 1):
-            v = P[E + dy:E + dy + h, E + dx:E + dx + w]
+            v = P[H + y0 + dy:H + y1 + dy, H + x0 + dx:H + x1 + dx]
             res += (c2d * (v - u)) * dh2
     return u + res * dt
 
@@ -59,6 +61,7 @@ def _worker(rank, world, port, case, q):
         from oracle import oracle as O
         nx, ny, eps, nt, tiles, owner, split = (case[k] for k in
                                                 ("nx", "ny", "eps", "nt", "tiles", "owner", "split"))
+        two = case.get("two_step", False)
         k, dh = 1.0, 1.0 / nx
         dt = eps ** 4 * dh * dh / (8 * k * N.disk_count(eps))
         p = O.params(nx, ny, eps, k, dt, dh, 0)
@@ -66,23 +69,34 @@ def _worker(rank, world, port, case, q):
         ref = O.run(p, nt, u0)
         c2d = (k * 8) / (eps * dh) ** 4
         lens = _lens(eps)
-        blocks = N.block_plan(nx, ny, eps, tiles, owner, world, split)
-        allp = np.concatenate([N.halo_plan(nx, ny, eps, tiles, owner, r, world, split)
-                               for r in range(world)] or [np.zeros((0, 8), np.int64)])
         E = eps
+        # the plans nlh_create builds: production fast mode (two steps per
+        # pass, 2*eps halo) or the single-step exact kernel (eps halo)
+        kern = "auto" if two else "exact"
+        H = 2 * E if two else E
+        kw = dict(k=k, dt=dt, dh=dh, test=False, kernel=kern)
+        blocks = N.block_plan(nx, ny, eps, tiles, owner, world, split, **kw)
+        allp = np.concatenate([N.halo_plan(nx, ny, eps, tiles, owner, r, world, split, **kw)
+                               for r in range(world)] or [np.zeros((0, 8), np.int64)])
+        # the plan's pieces fill exactly an H-wide frame (checked per piece below)
+        for pc in allp:
+            src, dst, gx0, gy0, w, h, sb, db = (int(v) for v in pc)
+            _, _, bx0, by0, bw, bh = (int(v) for v in blocks[db])
+            assert bx0 - H <= gx0 and gx0 + w <= bx0 + bw + H
+            assert by0 - H <= gy0 and gy0 + h <= by0 + bh + H
         mine = {bi: b for bi, b in enumerate(blocks) if b[0] == rank}
         pad = {}
         for bi, b in mine.items():
             _, _, x0, y0, w, h = b
-            P = np.zeros((h + 2 * E, w + 2 * E))
-            P[E:E + h, E:E + w] = u0[y0:y0 + h, x0:x0 + w]
+            P = np.zeros((h + 2 * H, w + 2 * H))
+            P[H:H + h, H:H + w] = u0[y0:y0 + h, x0:x0 + w]
             pad[bi] = P
 
         def view(bi, gx0, gy0, w, h):
             _, _, x0, y0, _, _ = blocks[bi]
-            return pad[bi][E + gy0 - y0:E + gy0 - y0 + h, E + gx0 - x0:E + gx0 - x0 + w]
+            return pad[bi][H + gy0 - y0:H + gy0 - y0 + h, H + gx0 - x0:H + gx0 - x0 + w]
 
-        for _ in range(nt):
+        def exchange():
             reqs, recv = [], []
             for pc in allp:
                 src, dst, gx0, gy0, w, h, sb, db = (int(v) for v in pc)
@@ -99,15 +113,32 @@ def _worker(rank, world, port, case, q):
                 r.wait()
             for db, gx0, gy0, w, h, t in recv:
                 view(db, gx0, gy0, w, h)[...] = t.numpy()
+
+        t = 0
+        while t < nt:
+            exchange()
+            steps = 2 if (two and nt - t >= 2) else 1
             new = {}
             for bi, b in mine.items():
-                new[bi] = block_step(pad[bi], E, int(b[4]), int(b[5]), c2d, dh * dh, dt, lens)
+                _, _, bx0, by0, w, h = (int(v) for v in b)
+                if steps == 2:
+                    # pass: u^{t+1} on the block + an E ring (inside the
+                    # domain), then u^{t+2} on the block from it
+                    ex0, ey0 = max(-E, -bx0), max(-E, -by0)
+                    ex1, ey1 = min(w + E, nx - bx0), min(h + E, ny - by0)
+                    Q = np.zeros_like(pad[bi])
+                    Q[H + ey0:H + ey1, H + ex0:H + ex1] = block_step(pad[bi], H, ex0, ey0, ex1, ey1,
+                                                                     c2d, dh * dh, dt, lens, E)
+                    new[bi] = block_step(Q, H, 0, 0, w, h, c2d, dh * dh, dt, lens, E)
+                else:
+                    new[bi] = block_step(pad[bi], H, 0, 0, w, h, c2d, dh * dh, dt, lens, E)
             for bi, b in mine.items():
-                pad[bi][E:E + int(b[5]), E:E + int(b[4])] = new[bi]
+                pad[bi][H:H + int(b[5]), H:H + int(b[4])] = new[bi]
+            t += steps
         ok, nblk = True, 0
         for bi, b in mine.items():
             _, _, x0, y0, w, h = (int(v) for v in b)
-            ok &= bool(np.array_equal(pad[bi][E:E + h, E:E + w], ref[y0:y0 + h, x0:x0 + w]))
+            ok &= bool(np.array_equal(pad[bi][H:H + h, H:H + w], ref[y0:y0 + h, x0:x0 + w]))
             nblk += 1
         q.put((rank, ok, nblk))
     finally:
@@ -121,8 +152,16 @@ CASES = [
     dict(name="eps > tile, split tiles", nx=30, ny=20, eps=7, nt=2, tiles=(6, 4), owner=None, split=True, world=3),
     dict(name="25s_8n map folded to 3 ranks", nx=50, ny=50, eps=4, nt=3, tiles=(5, 5), owner="25s_8n",
          split=False, world=3),
-    # bench.py --gpus 8 layout (decomposition(8) = 4x2 blocks, one per rank, locidx owners)
-    dict(name="bench N=8 layout 4x2", nx=64, ny=32, eps=6, nt=3, tiles=(4, 2), owner=None, split=False, world=8),
+    # bench.py --gpus 8 layout (decomposition(8) = 2x4 blocks, npx=2 npy=4, one per rank)
+    dict(name="bench N=8 layout 2x4", nx=32, ny=64, eps=6, nt=3, tiles=(2, 4), owner=None, split=False, world=8),
+    # the production two-step plan: 2*eps halo, one exchange per two steps
+    # (odd nt: the last step single), as nlh_create builds it
+    dict(name="two-step 2x2 locidx", nx=48, ny=40, eps=4, nt=5, tiles=(2, 2), owner=None, split=False,
+         world=2, two_step=True),
+    dict(name="two-step 25s_8n on 8 ranks", nx=50, ny=50, eps=3, nt=4, tiles=(5, 5), owner="25s_8n",
+         split=False, world=8, two_step=True),
+    dict(name="two-step eps > tile", nx=30, ny=24, eps=5, nt=4, tiles=(6, 4), owner=None, split=True,
+         world=3, two_step=True),
 ]
 
 
@@ -167,17 +206,23 @@ def test_block_plan_covers_lattice():
         assert (cover == 1).all()
 
 
-def test_halo_plan_covers_halo_exactly():
+@pytest.mark.parametrize("kernel,test,width", [("exact", False, 1), ("auto", True, 1), ("auto", False, 2)])
+def test_halo_plan_covers_halo_exactly(kernel, test, width):
+    """The plan's pieces fill exactly the halo frame of each block: eps wide
+    for the single-step kernels (exact, and the fast test mode), 2*eps for the
+    two-step production pass -- the width nlh_create resolves."""
     nx, ny, eps, tiles, world = 60, 48, 7, (6, 4), 3
-    b = N.block_plan(nx, ny, eps, tiles, None, world, True)
+    kw = dict(k=1.0, dt=eps ** 4 / (nx * nx * 8.0 * N.disk_count(eps)), dh=1.0 / nx, test=test, kernel=kernel)
+    H = width * eps
+    b = N.block_plan(nx, ny, eps, tiles, None, world, True, **kw)
     for rank in range(world):
-        pcs = N.halo_plan(nx, ny, eps, tiles, None, rank, world, True)
+        pcs = N.halo_plan(nx, ny, eps, tiles, None, rank, world, True, **kw)
         for bi, blk in enumerate(b):
             if blk[0] != rank:
                 continue
             _, _, x0, y0, w, h = blk
             need = np.zeros((ny, nx), np.int32)
-            need[max(0, y0 - eps):min(ny, y0 + h + eps), max(0, x0 - eps):min(nx, x0 + w + eps)] = 1
+            need[max(0, y0 - H):min(ny, y0 + h + H), max(0, x0 - H):min(nx, x0 + w + H)] = 1
             need[y0:y0 + h, x0:x0 + w] = 0
             got = np.zeros_like(need)
             for src, dst, gx0, gy0, pw, ph, sb, db in pcs:

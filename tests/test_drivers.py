@@ -87,7 +87,8 @@ def test_logging_csv_vtu(tmp_path, oracle):
     run_dir.mkdir()
     (tmp_path / "out_csv").mkdir()
     (tmp_path / "out_vtk").mkdir()
-    run("2d_nonlocal_serial", ["--test", "--cmp", "false", "--nt", "11", "--nlog", "5"], cwd=run_dir)
+    run("2d_nonlocal_serial", ["--test", "--cmp", "false", "--nt", "11", "--nlog", "5", "--kernel", "exact"],
+        cwd=run_dir)
     rows = open(tmp_path / "out_csv" / "simulate_2d.csv").read().splitlines()
     assert len(rows) == 3 * 2500  # t = 0, 5, 10
     assert rows[0].startswith("0,0,0,")

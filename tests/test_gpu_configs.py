@@ -1,0 +1,154 @@
+"""GPU: BASELINE.json's multi-GPU configurations at full size on one MI355X,
+and long-run parity.
+
+* C3 (32768^2, eps=8, npx=2 x npy=4 blocks of 16384 x 8192): the eight
+  blocks of the 8-GPU layout on one device, every halo piece packed, sent
+  through ncclSend/ncclRecv (to self, NLH_RCCL_SELF) and unpacked -- the
+  production two-step pass, checked per node against the bit-parity kernel
+  k_exact on one block (bitwise equal to the reference's per-term order on
+  every oracle-sized case), plus the bitwise linearity step(2u) = 2 step(u).
+* C5 uneven (tests/load_balance_25s_8n.txt: 5 x 5 tiles of 9216^2 over 8
+  owners, 1-7 tiles each, 2.1 G nodes = 16384^2 per GPU on average): the
+  owners' blocks on one device (NLH_VIRTUAL_RANKS=8), pieces between owners
+  over RCCL, checked against k_exact.
+* Long runs: the fast kernels over 1000 steps against the reference's own
+  known answers (long_runs_eps8: L2 of the reference
+  serial solver at 64^2 and 96^2) and the two-step pass against the oracle.
+
+Tolerances as tests/test_gpu_parity.py: 1e-12 of field scale per node, L2
+within 1e-10 relative.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, read_input
+
+import nonlocalheatequation_amd as N
+
+pytestmark = pytest.mark.gpu
+
+with open(os.path.join(ROOT, "tests", "golden", "known_answers.json")) as f:
+    KNOWN = json.load(f)
+
+
+def _dt(eps, dh, k=1.0):
+    return eps ** 4 * dh * dh / (8 * k * N.disk_count(eps))
+
+
+def _max_abs_diff(a, b, rows=2048):
+    """max |a - b| and max |b| without full-size temporaries."""
+    d = s = 0.0
+    for y in range(0, a.shape[0], rows):
+        x = a[y:y + rows]
+        r = b[y:y + rows]
+        d = max(d, float(np.max(np.abs(x - r))))
+        s = max(s, float(np.max(np.abs(r))))
+    return d, s
+
+
+def _bitwise_double(a, b, rows=2048):
+    for y in range(0, a.shape[0], rows):
+        if not np.array_equal((2.0 * a[y:y + rows]).view(np.uint64), b[y:y + rows].view(np.uint64)):
+            return False
+    return True
+
+
+def _run(nx, ny, eps, nt, kernel, u0=None, tiles=(1, 1), split=False, owner=None, test=False, ic_scale=None):
+    dh = 1.0 / nx
+    with N.Solver(nx, ny, eps, 1.0, _dt(eps, dh), dh, test=test, kernel=kernel, tiles=tiles,
+                  split_tiles=split, owner=owner) as s:
+        if u0 is None:
+            s.test_init()
+        else:
+            s.input_init(u0)
+        s.run(nt)
+        s.synchronize()
+        return s.field(), s.info()
+
+
+def test_c3_blocks_over_rccl_self(monkeypatch):
+    """C3's 2 x 4 layout of 16384 x 8192 blocks (8.6 GB per field) through the
+    RCCL transport, two two-step passes; vs k_exact per node, and linear."""
+    n, eps, nt = 32768, 8, 4
+    rng = np.random.default_rng(3)
+    u0 = np.empty((n, n))
+    for y in range(0, n, 4096):
+        u0[y:y + 4096] = rng.uniform(-1.0, 1.0, size=(4096, n))
+    monkeypatch.setenv("NLH_RCCL_SELF", "1")
+    uf, info = _run(n, n, eps, nt, "fast", u0, tiles=(2, 4), split=True)
+    assert info.nblocks == 8 and info.npeers == 1 and info.steps_per_pass == 2
+    assert info.halo_width == 2 * eps and info.halo_bytes_sent > 0
+    monkeypatch.delenv("NLH_RCCL_SELF")
+    ue, info_e = _run(n, n, eps, nt, "exact", u0)
+    assert info_e.kernel == N.KERNEL_EXACT and info_e.nblocks == 1
+    d, scale = _max_abs_diff(uf, ue)
+    assert d <= 1e-12 * scale, f"max |diff| {d} vs scale {scale}"
+    del ue
+    # linearity of the explicit step (test=0): every add, multiply and fma of
+    # the pass commutes with scaling by 2, so step(2u) == 2 step(u) bitwise
+    u0 *= 2.0
+    monkeypatch.setenv("NLH_RCCL_SELF", "1")
+    u2, _ = _run(n, n, eps, nt, "fast", u0, tiles=(2, 4), split=True)
+    assert _bitwise_double(uf, u2)
+
+
+def test_c5_uneven_owner_map_virtual_ranks(monkeypatch):
+    """C5's uneven case: tests/load_balance_25s_8n.txt over 5 x 5 tiles of
+    9216^2 (46080^2, 17 GB per field); each of the 8 owners' tiles merged into
+    its own blocks, pieces between owners over RCCL (to self).  One two-step
+    pass plus one single step (odd nt) from the test_init IC, vs k_exact."""
+    tok = read_input("load_balance_25s_8n.txt").split()
+    npx, npy = int(tok[2]), int(tok[3])
+    owner = [0] * (npx * npy)
+    vals = list(map(int, tok[5:]))
+    for i in range(npx * npy):
+        px, py, loc = vals[3 * i:3 * i + 3]
+        owner[px + py * npx] = loc
+    tile, eps, nt = 9216, 8, 3
+    n = tile * npx
+    monkeypatch.setenv("NLH_VIRTUAL_RANKS", "8")
+    uf, info = _run(n, n, eps, nt, "fast", None, tiles=(npx, npy), owner=owner)
+    plan = N.block_plan(n, n, eps, (npx, npy), owner, 8, False)
+    assert info.nblocks == len(plan) > 8 and info.npeers == 1 and info.halo_bytes_sent > 0
+    assert info.steps_per_pass == 2
+    monkeypatch.delenv("NLH_VIRTUAL_RANKS")
+    ue, _ = _run(n, n, eps, nt, "exact", None)
+    d, scale = _max_abs_diff(uf, ue)
+    assert d <= 1e-12 * scale, f"max |diff| {d} vs scale {scale}"
+
+
+@pytest.mark.parametrize("kernel", ["fast", "auto", "exact"])
+@pytest.mark.parametrize("case", range(len(KNOWN["long_runs_eps8"])))
+def test_long_run_l2_known_answers(kernel, case):
+    """1000 test-mode steps at eps=8 (64^2, 96^2): the L2 error of the
+    reference serial solver itself within 1e-10
+    relative -- the fast kernels' reordered sums must not drift."""
+    ka = KNOWN["long_runs_eps8"][case]
+    nx, ny, nt, eps = ka["nx"], ka["ny"], ka["nt"], ka["eps"]
+    dh = 1.0 / nx
+    with N.Solver(nx, ny, eps, 1.0, _dt(eps, dh), dh, test=True, kernel=kernel) as s:
+        s.test_init()
+        s.do_work(nt)
+        info = s.info()
+        l2 = s.error_l2
+    assert info.kernel == (N.KERNEL_EXACT if kernel == "exact" else N.KERNEL_FAST)
+    tol = 1e-13 if kernel == "exact" else 1e-10
+    assert abs(l2 - ka["l2"]) <= tol * ka["l2"], f"l2 {l2!r} vs {ka['l2']!r}: rel {abs(l2 - ka['l2']) / ka['l2']:.3e}"
+
+
+def test_long_run_two_step_pass_vs_oracle(oracle):
+    """1000 production steps (500 two-step passes) at 256^2, eps=8, random IC,
+    vs the oracle per node."""
+    nx = ny = 256
+    eps, nt = 8, 1000
+    dh = 1.0 / nx
+    dt = _dt(eps, dh)
+    u0 = np.random.default_rng(1000).uniform(-1.0, 1.0, size=(ny, nx))
+    u, info = _run(nx, ny, eps, nt, "fast", u0)
+    assert info.steps_per_pass == 2
+    ref = oracle.run(oracle.params(nx, ny, eps, 1.0, dt, dh, 0), nt, u0)
+    scale = np.max(np.abs(ref))
+    assert np.max(np.abs(u - ref)) <= 1e-12 * scale

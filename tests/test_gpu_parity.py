@@ -81,14 +81,20 @@ def test_fast_test_mode_l2(oracle, row):
 
 @pytest.mark.parametrize("row", range(len(ASYNC_ROWS)))
 def test_tiled_rows_single_gpu(oracle, row):
-    """tests/2d_async.txt rows (np x np tiles) map onto one GPU block."""
+    """tests/2d_async.txt rows (np x np tiles) map onto one GPU block: the
+    exact kernel bitwise, AUTO (the fast kernel with the precomputed source,
+    also in test mode) within the north-star tolerances."""
     r = ASYNC_ROWS[row]
     u_ref, l2_ref, li_ref = _oracle_run(oracle, r, True)
-    u, l2, li, info = _gpu_run(r, True, "auto")
+    u, l2, li, info = _gpu_run(r, True, "exact")
     assert info.nblocks == 1
     assert np.array_equal(u, u_ref)
     assert li == li_ref
     assert l2 / (r.nx * r.ny) <= 1e-6
+    u, l2, li, info = _gpu_run(r, True, "auto")
+    assert info.kernel == N.KERNEL_FAST
+    assert np.max(np.abs(u - u_ref)) <= 1e-12 * np.max(np.abs(u_ref))
+    assert abs(l2 - l2_ref) <= 1e-10 * l2_ref
 
 
 FAST_EPS = list(range(1, 17)) + [20, 24, 32]
