@@ -17,7 +17,7 @@ INC     := -Iinclude -I$(CSRC)
 HIPFLAGS := --offload-arch=$(ARCH) -O3 $(CXXSTD) -fPIC $(WARN) $(INC) -munsafe-fp-atomics
 HOSTFLAGS := -O2 $(CXXSTD) -fPIC $(WARN) $(INC) -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include
 
-FAST_UNITS := $(sort $(wildcard $(CSRC)/nlh_fast_e*.hip $(CSRC)/nlh_pair_e*.hip))
+FAST_UNITS := $(sort $(wildcard $(CSRC)/nlh_fast_e*.hip $(CSRC)/nlh_pair_e*.hip $(CSRC)/nlh_wide_e*.hip))
 FAST_OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(FAST_UNITS))
 LIB_OBJS := $(OBJDIR)/nlh_kernels.o $(FAST_OBJS) $(OBJDIR)/nlh_api.o $(OBJDIR)/nlh_plan.o
 # the fast kernel is fully unrolled over 2E+1 rows; lift LLVM's pragma-unroll
@@ -35,15 +35,19 @@ oracle:
 $(OBJDIR) $(LIBDIR) $(BINDIR):
 	mkdir -p $@
 
-KHDRS := $(CSRC)/nlh_device.h $(CSRC)/nlh_kernel_common.h $(CSRC)/nlh_fast.h $(CSRC)/nlh_pair.h
+CHDRS := $(CSRC)/nlh_device.h $(CSRC)/nlh_kernel_common.h
+KHDRS := $(CHDRS) $(CSRC)/nlh_fast.h $(CSRC)/nlh_pair.h $(CSRC)/nlh_wide.h
 
 $(OBJDIR)/nlh_kernels.o: $(CSRC)/nlh_kernels.hip $(KHDRS) | $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(OBJDIR)/nlh_fast_%.o: $(CSRC)/nlh_fast_%.hip $(KHDRS) | $(OBJDIR)
+$(OBJDIR)/nlh_fast_%.o: $(CSRC)/nlh_fast_%.hip $(CHDRS) $(CSRC)/nlh_fast.h | $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) $(UNROLL) -c $< -o $@
 
-$(OBJDIR)/nlh_pair_%.o: $(CSRC)/nlh_pair_%.hip $(KHDRS) | $(OBJDIR)
+$(OBJDIR)/nlh_pair_%.o: $(CSRC)/nlh_pair_%.hip $(CHDRS) $(CSRC)/nlh_pair.h | $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) $(UNROLL) -c $< -o $@
+
+$(OBJDIR)/nlh_wide_%.o: $(CSRC)/nlh_wide_%.hip $(CHDRS) $(CSRC)/nlh_wide.h | $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) $(UNROLL) -c $< -o $@
 
 $(OBJDIR)/nlh_api.o: $(CSRC)/nlh_api.cpp $(CSRC)/nlh_device.h $(CSRC)/nlh_plan.h include/nlh.h | $(OBJDIR)

@@ -63,6 +63,7 @@ int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 struct Resolved {
   int kernel = NLH_KERNEL_EXACT;
   bool pair = false;  // two steps per pass (nlh_pair.h)
+  bool wide = false;  // large-horizon single-step kernel (nlh_wide.h)
   int halo = 0;       // eps, or 2*eps with pair
   int ablate = 0;     // diagnostics only (NLH_ABLATE)
 };
@@ -80,14 +81,21 @@ int resolve_config(const nlh_params &p, Resolved &r) {
       return fail(NLH_ERR_UNSUPPORTED, "fast kernel not instantiated for eps=" + std::to_string(E));
     kern = NLH_KERNEL_EXACT;
   }
+  const double alpha = ((p.k * 8) / pow(p.eps * p.dh, 4)) * (p.dh * p.dh) * p.dt;
+  const bool fold_ok = alpha != 0.0 && std::isfinite(1.0 / alpha);  // centre fold usable
+  if (kern == NLH_KERNEL_FAST && nlh::wide_supported(E) && !fold_ok) {
+    // the large-horizon kernel folds the centre term (1/alpha - N)
+    if (p.kernel == NLH_KERNEL_FAST)
+      return fail(NLH_ERR_UNSUPPORTED, "fast kernel for eps > 16 needs k*dt*dh != 0");
+    kern = NLH_KERNEL_EXACT;
+  }
   r.kernel = kern;
+  r.wide = kern == NLH_KERNEL_FAST && nlh::wide_supported(E);
   r.ablate = 0;
   if (const char *ab = std::getenv("NLH_ABLATE")) r.ablate = std::atoi(ab);
   // production fast mode advances two steps per pass; the source term of the
   // test mode and a zero alpha (no centre fold) keep the single-step kernels
-  const double alpha = ((p.k * 8) / pow(p.eps * p.dh, 4)) * (p.dh * p.dh) * p.dt;
-  r.pair = kern == NLH_KERNEL_FAST && !p.test && nlh::pair_supported(E) && alpha != 0.0 &&
-           std::isfinite(1.0 / alpha) && r.ablate == 0;
+  r.pair = kern == NLH_KERNEL_FAST && !p.test && nlh::pair_supported(E) && fold_ok && r.ablate == 0;
   if (const char *pe = std::getenv("NLH_PAIR")) r.pair = r.pair && std::atoi(pe) != 0;
   r.halo = r.pair ? 2 * E : E;
   return NLH_OK;
@@ -133,10 +141,11 @@ struct nlh_solver {
   int kernel = NLH_KERNEL_EXACT;
   int fast_r = 2;  // columns per lane of the fast kernel (NLH_FAST_R=1|2|4: 64/128/256-column strips)
   bool pair = false;  // two steps per pass (nlh_pair.h); production fast mode (NLH_PAIR=0 disables)
+  bool wide = false;  // k_wide (nlh_wide.h) for eps 17..32
   int halo = 0;       // halo rows/columns held per block: eps, or 2*eps with pair
   int ablate = 0;     // diagnostics only (NLH_ABLATE), never set in production
   int pair_ablate = 0;  // diagnostics only (NLH_PAIR_ABLATE)
-  int pair_split = 1;  // 1 k_pair_split (default), 0 k_pair, 2 k_pair_mw (NLH_PAIR_SPLIT)
+  int pair_split = 1;  // 1 k_pair_split (default), 0 k_pair, 2 k_pair_mw, 3 k_pair_pf (NLH_PAIR_SPLIT)
   hipStream_t s_main = nullptr, s_comm = nullptr, s_band = nullptr;
   hipEvent_t ev_ready = nullptr, ev_halo = nullptr, ev_band = nullptr, ev_int = nullptr;
   bool halo_fresh = false;  // the current field's halo holds its neighbours' values
@@ -290,6 +299,11 @@ int build_rectlists(nlh_solver *s, int kind) {
         if (seg == 16) break;
       }
       seg_h = own ? s->p.seg_rows : (int)best;
+    } else if (s->wide) {
+      // k_wide: one-wave workgroups at two waves per SIMD (8 per CU, 214
+      // VGPRs at E = 32; profiles/r02/wide_bench_*), one round
+      seg_h = own ? s->p.seg_rows
+                  : (int)std::max<int64_t>(2 * E, ceil_div(strip_rows, (int64_t)8 * s->cus));
     } else {
       seg_h = own ? s->p.seg_rows
                   : (int)std::max<int64_t>(nlh::fast_seg_min(E), ceil_div(strip_rows, 1024));
@@ -459,7 +473,9 @@ int launch_stencil(nlh_solver *s, const std::vector<nlh::RectList> &v, hipStream
   for (const auto &rl : v) {
     if (rl.nwork == 0) continue;
     int rc;
-    if (s->kernel == NLH_KERNEL_FAST && !test && s->ablate)
+    if (s->wide)
+      rc = nlh::launch_wide(rl, s->sc, test, st);
+    else if (s->kernel == NLH_KERNEL_FAST && !test && s->ablate)
       rc = nlh::launch_fast_ablation(rl, s->sc, s->ablate, st);
     else if (s->kernel == NLH_KERNEL_FAST)
       rc = nlh::launch_fast(rl, s->sc, test, s->fast_r, st);
@@ -695,6 +711,7 @@ int create_impl(const nlh_params *pin, nlh_solver *s) {
   s->fast_r = nlh::fast_lanes_cols(E, s->fast_r);
   s->ablate = rv.ablate;
   s->pair = rv.pair;
+  s->wide = rv.wide;
   if (const char *pa = std::getenv("NLH_PAIR_ABLATE")) s->pair_ablate = std::atoi(pa);
   if (const char *fb = std::getenv("NLH_FORCE_BANDS")) s->force_bands = std::atoi(fb) != 0;
   if (const char *rs = std::getenv("NLH_RCCL_SELF")) s->rccl_self = p.nranks == 1 && std::atoi(rs) != 0;
@@ -704,7 +721,7 @@ int create_impl(const nlh_params *pin, nlh_solver *s) {
   int prio_lo = 0, prio_hi = 0;  // NLH_COMM_PRIO=1: exchange + band streams at the highest priority
   if (const char *cp = std::getenv("NLH_COMM_PRIO"))
     if (std::atoi(cp) != 0) HIP_TRY(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
-  if (const char *ps = std::getenv("NLH_PAIR_SPLIT")) s->pair_split = std::min(2, std::max(0, std::atoi(ps)));
+  if (const char *ps = std::getenv("NLH_PAIR_SPLIT")) s->pair_split = std::min(3, std::max(0, std::atoi(ps)));
   if (s->pair_ablate >= 10000) s->pair_split = 1;
   s->halo = rv.halo;
   s->plan = nlh::make_plan(p.nx, p.ny, s->halo, tx, ty, s->owner, p.split_tiles == 0);
@@ -748,7 +765,7 @@ int create_impl(const nlh_params *pin, nlh_solver *s) {
   s->sc.dt = p.dt;
   s->sc.alpha = s->sc.c2d * s->sc.dh2 * p.dt;
   s->sc.nf = (double)s->disk;
-  s->sc.kc = s->pair ? 1.0 / s->sc.alpha - s->sc.nf : 0.0;
+  s->sc.kc = (s->pair || s->wide) ? 1.0 / s->sc.alpha - s->sc.nf : 0.0;
   s->sc.sxt = s->d_sxt;
   s->sc.syt = s->d_syt;
   s->sc.lens = s->d_lens;
@@ -1124,8 +1141,9 @@ int nlh_get_info(const nlh_solver *s, nlh_info *info) {
   info->device_bytes = s->device_bytes;
   info->halo_width = s->halo;
   info->steps_per_pass = s->pair ? 2 : 1;
-  const char *pk = s->pair ? (s->pair_split == 2 ? "k_pair_mw" : s->pair_split == 1 ? "k_pair_split" : "k_pair")
-                           : (s->kernel == NLH_KERNEL_FAST ? "k_fast" : "k_exact");
+  const char *pk = s->pair ? (s->pair_split == 3 ? "k_pair_pf" : s->pair_split == 2 ? "k_pair_mw"
+                              : s->pair_split == 1 ? "k_pair_split" : "k_pair")
+                           : s->wide ? "k_wide" : (s->kernel == NLH_KERNEL_FAST ? "k_fast" : "k_exact");
   std::snprintf(info->pass_kernel, sizeof(info->pass_kernel), "%s", pk);
   std::snprintf(info->arch, sizeof(info->arch), "%s", s->arch);
   return NLH_OK;

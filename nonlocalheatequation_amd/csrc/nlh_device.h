@@ -53,7 +53,7 @@ struct StepConst {
   int64_t nx, ny;  // global lattice
   int32_t E;
   int32_t seg_h;   // fast kernel segment height
-  double kc;       // 1/alpha - N  (pair kernel centre fold)
+  double kc;       // 1/alpha - N  (centre fold: pair and wide kernels)
   int32_t seg_pair;  // pair kernel segment height
   int32_t pad_;
 };
@@ -87,6 +87,10 @@ int fast_strip_width(int E, int want_r);  // 64*R columns per strip
 int fast_seg_min(int E);                  // smallest sensible segment height
 // Work-item counts are filled into rl by the caller (wg_begin/nwork).
 int launch_fast(const RectList &rl, const StepConst &c, bool test, int want_r, void *stream);
+// large horizons (nlh_wide.h, eps in [17, 32]): single-step, 64-column strips,
+// centre fold (needs kc), production and fast test mode
+bool wide_supported(int E);
+int launch_wide(const RectList &rl, const StepConst &c, bool test, void *stream);
 // two-step pass (nlh_pair.h): production mode, eps in [1, 16]
 bool pair_supported(int E);
 int pair_strip_width(int E);  // output columns per strip: 128 - 2E

@@ -32,6 +32,7 @@
 
 #include "nlh_fast.h"
 #include "nlh_pair.h"
+#include "nlh_wide.h"
 #include "nlh_kernel_common.h"
 
 namespace nlh {
@@ -171,8 +172,8 @@ static int check_launch() {
 
 // Fast-kernel variants, instantiated in nlh_fast_e*.hip (parallel build):
 //   E = 1..16        128-column strips (R = 2); E <= 8 also 256-column (R = 4)
-//   E = 20, 24, 32   64-column strips (R = 1) with the compact centre ring
-// Any other horizon runs k_exact.
+//                    and 64-column (R = 1)
+// E = 17..32 run k_wide (nlh_wide.h); larger horizons run k_exact.
 #define NLH_FAST_EXTERN(E, R)                                                            \
   extern template int launch_fast_er<E, R, true>(const RectList &, const StepConst &, hipStream_t); \
   extern template int launch_fast_er<E, R, false>(const RectList &, const StepConst &, hipStream_t);
@@ -186,7 +187,32 @@ NLH_FAST_EXTERN(1, 1) NLH_FAST_EXTERN(2, 1) NLH_FAST_EXTERN(3, 1) NLH_FAST_EXTER
 NLH_FAST_EXTERN(5, 1) NLH_FAST_EXTERN(6, 1) NLH_FAST_EXTERN(7, 1) NLH_FAST_EXTERN(8, 1)
 NLH_FAST_EXTERN(9, 1) NLH_FAST_EXTERN(10, 1) NLH_FAST_EXTERN(11, 1) NLH_FAST_EXTERN(12, 1)
 NLH_FAST_EXTERN(13, 1) NLH_FAST_EXTERN(14, 1) NLH_FAST_EXTERN(15, 1) NLH_FAST_EXTERN(16, 1)
-NLH_FAST_EXTERN(20, 1) NLH_FAST_EXTERN(24, 1) NLH_FAST_EXTERN(32, 1)
+
+// Large horizons (nlh_wide.h), instantiated in nlh_wide_e*.hip for E = 17..32
+#define NLH_WIDE_EXTERN(E)                                                             \
+  extern template int launch_wide_e<E, true>(const RectList &, const StepConst &, hipStream_t); \
+  extern template int launch_wide_e<E, false>(const RectList &, const StepConst &, hipStream_t);
+NLH_WIDE_EXTERN(17) NLH_WIDE_EXTERN(18) NLH_WIDE_EXTERN(19) NLH_WIDE_EXTERN(20)
+NLH_WIDE_EXTERN(21) NLH_WIDE_EXTERN(22) NLH_WIDE_EXTERN(23) NLH_WIDE_EXTERN(24)
+NLH_WIDE_EXTERN(25) NLH_WIDE_EXTERN(26) NLH_WIDE_EXTERN(27) NLH_WIDE_EXTERN(28)
+NLH_WIDE_EXTERN(29) NLH_WIDE_EXTERN(30) NLH_WIDE_EXTERN(31) NLH_WIDE_EXTERN(32)
+
+bool wide_supported(int E) { return E >= 17 && E <= 32; }
+
+int launch_wide(const RectList &rl, const StepConst &c, bool test, void *stream) {
+  hipStream_t st = (hipStream_t)stream;
+  switch (c.E) {
+#define NLH_CASEW(EE) \
+  case EE:            \
+    return test ? launch_wide_e<EE, true>(rl, c, st) : launch_wide_e<EE, false>(rl, c, st);
+    NLH_CASEW(17) NLH_CASEW(18) NLH_CASEW(19) NLH_CASEW(20) NLH_CASEW(21) NLH_CASEW(22)
+    NLH_CASEW(23) NLH_CASEW(24) NLH_CASEW(25) NLH_CASEW(26) NLH_CASEW(27) NLH_CASEW(28)
+    NLH_CASEW(29) NLH_CASEW(30) NLH_CASEW(31) NLH_CASEW(32)
+#undef NLH_CASEW
+    default:
+      return -1;
+  }
+}
 
 extern template int launch_fast_abl<8, 2, 0, 6>(const RectList &, const StepConst &, hipStream_t);
 extern template int launch_fast_abl<8, 2, 1, 6>(const RectList &, const StepConst &, hipStream_t);
@@ -278,7 +304,7 @@ int launch_pair(const RectList &rl, const StepConst &c, int variant, void *strea
   }
 }
 
-bool fast_supported(int E) { return (E >= 1 && E <= 16) || E == 20 || E == 24 || E == 32; }
+bool fast_supported(int E) { return E >= 1 && E <= 32; }
 
 int fast_lanes_cols(int E, int want_r) {
   if (E > 16 || want_r == 1) return 1;
@@ -303,7 +329,6 @@ int launch_fast(const RectList &rl, const StepConst &c, bool test, int want_r, v
   NLH_CASE(1, 1) NLH_CASE(2, 1) NLH_CASE(3, 1) NLH_CASE(4, 1) NLH_CASE(5, 1) NLH_CASE(6, 1)
   NLH_CASE(7, 1) NLH_CASE(8, 1) NLH_CASE(9, 1) NLH_CASE(10, 1) NLH_CASE(11, 1) NLH_CASE(12, 1)
   NLH_CASE(13, 1) NLH_CASE(14, 1) NLH_CASE(15, 1) NLH_CASE(16, 1)
-  NLH_CASE(20, 1) NLH_CASE(24, 1) NLH_CASE(32, 1)
 #undef NLH_CASE
   return -1;
 }

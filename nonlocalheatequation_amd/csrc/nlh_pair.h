@@ -108,7 +108,12 @@ __device__ __forceinline__ void pair_scatter(const double (&w)[2 * E + 2], doubl
 }
 
 // ABL (diagnostics only, NLH_PAIR_ABLATE): 0 = production, 2 = no HBM
-// traffic (no DMA, no stores; same instruction stream otherwise)
+// traffic (no DMA, no stores; same instruction stream otherwise); k_pair_split
+// also: 4 = windows from registers (no LDS window reads), 8 = no s_barrier,
+// 16 = no u^{t+1} LDS writes, 32 = no per-row range checks (rows past the
+// segment end computed too), 64 = no vmcnt waits for the DMA'd rows, 128 = no
+// output stores, 256 = no DMA, 512 = non-temporal stores, 1024 = temporal
+// (non-nt) DMA (timing decompositions; results meaningless except 512/1024)
 template <int E, int D, int ABL = 0>
 __global__ __launch_bounds__(64, (E <= 9 ? 2 : 1)) void k_pair(RectList L, StepConst C) {
   constexpr int R = 2;
@@ -314,7 +319,24 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
 
   // s_barrier with every LDS access of this wave completed first; the asm
   // "memory" clobber also keeps the compiler from moving LDS accesses across
-  auto row_barrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+  auto row_barrier = [] {
+    if constexpr ((ABL & 8) != 0)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // ablation: no s_barrier
+    else
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  };
+  // ablation ABL & 4: windows from registers instead of LDS (opaque values)
+  auto window = [&](const double *p, double (&w)[NW]) {
+    if constexpr ((ABL & 4) != 0) {
+#pragma unroll
+      for (int k = 0; k < NW; ++k) {
+        w[k] = (double)(lane + k);
+        asm volatile("" : "+v"(w[k]));
+      }
+    } else {
+      pair_window<E, R>(p, w);
+    }
+  };
 
   double acc[R][P];
 #pragma unroll
@@ -341,11 +363,12 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
         constexpr int q = decltype(qc)::value;
         constexpr int so = (q + E + 1) % P;
         const int i = b + q;
-        if (i >= n_in) return;
+        if constexpr ((ABL & 32) == 0)
+          if (i >= n_in) return;
         double w[NW];
-        pair_window<E, R>(ring + ((bs + q) & (K - 1)) * RW + R * lane, w);
+        window(ring + ((bs + q) & (K - 1)) * RW + R * lane, w);
         pair_scatter<E, q>(w, acc, kc);
-        if (i >= 2 * E) {
+        if ((ABL & 32) != 0 || i >= 2 * E) {
           const int m = i - 2 * E;
           const int gy = gy1first + ydir * m;
           double v0 = mcol[0] * acc[0][so];
@@ -354,9 +377,13 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
             v0 = 0.0;
             v1 = 0.0;
           }
-          *reinterpret_cast<double2 *>(u1buf + (m & (U1R - 1)) * U1W + R * lane) = make_double2(v0, v1);
+          if constexpr ((ABL & 16) != 0)
+            asm volatile("" ::"v"(v0), "v"(v1));  // ablation: no u^{t+1} LDS write
+          else
+            *reinterpret_cast<double2 *>(u1buf + (m & (U1R - 1)) * U1W + R * lane) = make_double2(v0, v1);
         }
-        if ((i & (B - 1)) == B - 1) row_barrier();
+        if constexpr ((ABL & 40) != 40)
+          if ((i & (B - 1)) == B - 1) row_barrier();
       };
       static_for<P>(body);
       bs = (bs + P) & (K - 1);
@@ -370,8 +397,14 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
     const uint32_t lring = __builtin_amdgcn_readfirstlane(lds_addr(ring));
     int row = 0;  // next u^t row to fetch (clamped at the last one)
     auto issue = [&](int slot) {
-      if (!(ABL & 2)) dma_chunks<NCH>(gnext, lring + slot * RW * 8, lane);
-      if (++row < n_in) gnext += stride;
+      if constexpr ((ABL & 1024) != 0)  // ablation: temporal (non-nt) DMA
+        dma_chunks<NCH, false, false>(gnext, lring + slot * RW * 8, lane);
+      else if (!(ABL & 2) && !(ABL & 256))
+        dma_chunks<NCH>(gnext, lring + slot * RW * 8, lane);
+      if constexpr ((ABL & 32) != 0)
+        gnext += stride;
+      else if (++row < n_in)
+        gnext += stride;
     };
 #pragma unroll
     for (int s = 0; s < DT; ++s) issue(s);
@@ -389,6 +422,10 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
     // begun, iteration 4E+B; more outstanding only makes the wait longer)
     auto block_end = [&](int j) {
       if ((j & (B - 1)) != B - 1) return;
+      if constexpr ((ABL & 64) != 0) {
+        row_barrier();  // ablation: no wait for the DMA'd rows
+        return;
+      }
       if (j - D >= 4 * E + B)
         wait_vmcnt<D * G + D + 1>();
       else
@@ -409,15 +446,201 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
         constexpr int q2 = ((q + 1 - B) % P + P) % P;  // slot of row m2 = i - 2E - B
         constexpr int so = (q2 + E + 1) % P;
         const int i = b + q;
-        if (i > i_last) return;
+        if constexpr ((ABL & 32) == 0)
+          if (i > i_last) return;
         issue((bs + q + DT) & (K - 1));  // u^t row i+DT (clamped; never a slot wave 0 still reads)
         // u^{t+1} row m2 = i - 2E - B (m2 mod P == q2); rows m2 < 0 are LDS
         // garbage that only reaches accumulators of rows never emitted, each
         // assigned afresh before use
         const int m2 = i - 2 * E - B;
         double w2[NW];
-        pair_window<E, R>(u1buf + (m2 & (U1R - 1)) * U1W + R * lane, w2);
+        window(u1buf + (m2 & (U1R - 1)) * U1W + R * lane, w2);
         pair_scatter<E, q2>(w2, acc, kc);
+        if ((ABL & 32) != 0 || m2 >= 2 * E) {
+          const double o0 = alpha * acc[0][so];
+          const double o1 = alpha * acc[1][so];
+          double *dst = run + (int64_t)(yout0 + ydir * (m2 - 2 * E)) * pitch;
+          if constexpr ((ABL & 2) != 0 || (ABL & 128) != 0) {
+            asm volatile("" ::"v"(o0), "v"(o1));
+          } else if constexpr ((ABL & 512) != 0) {  // ablation: non-temporal stores
+            if (emit1) {
+              __builtin_nontemporal_store(o0, dst + xo);
+              __builtin_nontemporal_store(o1, dst + xo + 1);
+            } else if (emit0) {
+              __builtin_nontemporal_store(o0, dst + xo);
+            }
+          } else if (emit1) {
+            *reinterpret_cast<double2 *>(dst + xo) = make_double2(o0, o1);
+          } else if (emit0) {
+            dst[xo] = o0;
+          }
+        }
+        if constexpr ((ABL & 40) != 40) block_end(i);
+      };
+      static_for<P>(body);
+      bs = (bs + P) & (K - 1);
+    }
+    wait_vmcnt<0>();  // drain the clamped tail DMAs and the stores
+  }
+}
+
+// window buffer of row q of an unroll period of P rows: consecutive rows, the
+// wrap P-1 -> 0 included, never share one (three buffers for odd P)
+template <int P>
+__host__ __device__ constexpr int pf_slot(int q) {
+  return (P % 2 == 1 && q == P - 1) ? 2 : (q & 1);
+}
+
+// k_pair_pf: k_pair_split with the LDS window of the NEXT row read before the
+// math of the current one (software pipelining), so the ds_read latency of a
+// row hides behind the previous row's adds instead of stalling every row.
+// Row i+1 is prefetched unless row i ends a barrier block (its data is only
+// guaranteed after the barrier: then it is read right after it).  Same
+// arithmetic and order as k_pair_split: bitwise equal results.
+template <int E, int D, int ABL = 0, int B = kPairSplitB>
+__global__ __launch_bounds__(128, 2) void k_pair_pf(RectList L, StepConst C) {
+  constexpr int R = 2;
+  constexpr int P = 2 * E + 1;
+  constexpr int W1 = 64 * R;
+  constexpr int WO = W1 - 2 * E;
+  constexpr int NW = R + 2 * E;
+  constexpr int RW = W1 + 2 * E;
+  constexpr int NCH = RW / 2;
+  constexpr int DT = B + D;
+  constexpr int K = pow2_ceil(DT + B);
+  constexpr int G = (NCH + 63) / 64;
+  constexpr int U1W = W1 + 2 * E + 2;
+  constexpr int U1R = 2 * B;
+  static_assert((B & (B - 1)) == 0, "B must be a power of two");
+  static_assert(D * G + D + 1 < 64, "vmcnt range");
+  static_assert(WO >= 64, "strip too narrow for this eps");
+
+  __shared__ __attribute__((aligned(16))) double ring[K * RW + U1R * U1W];
+  double *const u1buf = ring + K * RW;
+
+  const int lane = (int)(threadIdx.x & 63);
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int work = xcd_remap(blockIdx.x, gridDim.x);
+  const int ri = find_rect(L, work);
+  const Rect &Rc = L.r[ri];
+  const int rx1 = Rc.x1, rgx0 = Rc.gx0, rgy0 = Rc.gy0;
+  const int local = work - Rc.wg_begin;
+  const int nstrip = Rc.nstrip;
+  const int strip = local % nstrip, seg = local / nstrip;
+  const int x0 = Rc.x0 + strip * WO;
+  const int seg_h = Rc.seg_rows;
+  const int Y0 = Rc.y0 + seg * seg_h;
+  const int Y1 = min(Y0 + seg_h, Rc.y1);
+  const int n_in = (Y1 - Y0) + 4 * E;
+  const int i_last = n_in - 1 + B;
+  const bool up = (seg & 1) != 0;
+  const int64_t pitch = Rc.pitch;
+  const int64_t stride = up ? -pitch : pitch;
+  const double alpha = C.alpha, kc = C.kc;
+  const int ydir = up ? -1 : 1;
+
+  auto row_barrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+
+  double acc[R][P];
+#pragma unroll
+  for (int c = 0; c < R; ++c)
+#pragma unroll
+    for (int j = 0; j < P; ++j) acc[c][j] = 0.0;
+  double wb[3][NW];  // window buffers (pf_slot); SSA values after unrolling
+
+  if (wave == 0) {
+    // ---- stage 1 on u^t row i
+    const int gny = (int)C.ny;
+    const int gy1first = rgy0 + (up ? (Y1 + E - 1) : (Y0 - E));
+    double mcol[R];
+#pragma unroll
+    for (int c = 0; c < R; ++c) {
+      const int gx = rgx0 + x0 - E + R * lane + c;
+      mcol[c] = (gx >= 0 && gx < (int)C.nx) ? alpha : 0.0;
+    }
+    auto ring_row = [&](int r) { return ring + (r & (K - 1)) * RW + R * lane; };
+    row_barrier();  // prologue: rows 0 .. B-1 landed
+    pair_window<E, R>(ring_row(0), wb[0]);
+    int bs = 0;     // b % K
+    for (int b = 0; b < n_in; b += P) {
+      auto body = [&](auto qc) {
+        constexpr int q = decltype(qc)::value;
+        constexpr int so = (q + E + 1) % P;
+        constexpr int cs = pf_slot<P>(q), ns = pf_slot<P>((q + 1) % P);
+        const int i = b + q;
+        if (i >= n_in) return;
+        const bool bend = (i & (B - 1)) == B - 1;
+        const bool more = i + 1 < n_in;
+        if (more && !bend) pair_window<E, R>(ring_row(bs + q + 1), wb[ns]);
+        pair_scatter<E, q>(wb[cs], acc, kc);
+        if (i >= 2 * E) {
+          const int m = i - 2 * E;
+          const int gy = gy1first + ydir * m;
+          double v0 = mcol[0] * acc[0][so];
+          double v1 = mcol[1] * acc[1][so];
+          if (gy < 0 || gy >= gny) {
+            v0 = 0.0;
+            v1 = 0.0;
+          }
+          *reinterpret_cast<double2 *>(u1buf + (m & (U1R - 1)) * U1W + R * lane) = make_double2(v0, v1);
+        }
+        if (bend) {
+          row_barrier();
+          if (more) pair_window<E, R>(ring_row(bs + q + 1), wb[ns]);
+        }
+      };
+      static_for<P>(body);
+      bs = (bs + P) & (K - 1);
+    }
+    for (int j = (i_last + 1) / B - n_in / B; j > 0; --j) row_barrier();
+  } else {
+    // ---- memory + stage 2 on u^{t+1} row m2 = i - 2E - B
+    const int yfirst = up ? (Y1 + 2 * E - 1) : (Y0 - 2 * E);
+    const double *gnext = Rc.u + (int64_t)yfirst * pitch + (x0 - 2 * E);
+    const uint32_t lring = __builtin_amdgcn_readfirstlane(lds_addr(ring));
+    int row = 0;
+    auto issue = [&](int slot) {
+      if (!(ABL & 2)) dma_chunks<NCH>(gnext, lring + slot * RW * 8, lane);
+      if (++row < n_in) gnext += stride;
+    };
+#pragma unroll
+    for (int s = 0; s < DT; ++s) issue(s);
+    wait_vmcnt<D * G>();
+    row_barrier();
+    const int xo = x0 + R * lane;
+    const bool emit0 = R * lane < WO && xo < rx1;
+    const bool emit1 = R * lane < WO && xo + 1 < rx1;
+    double *const run = Rc.un;
+    const int yout0 = up ? Y1 - 1 : Y0;
+    auto u1_row = [&](int m) { return u1buf + (m & (U1R - 1)) * U1W + R * lane; };
+    auto block_end = [&](int j) {
+      if ((j & (B - 1)) != B - 1) return;
+      if (j - D >= 4 * E + B)
+        wait_vmcnt<D * G + D + 1>();
+      else
+        wait_vmcnt<D * G>();
+      row_barrier();
+    };
+    for (int i = 0; i < P; ++i) {
+      issue((i + DT) & (K - 1));
+      block_end(i);
+    }
+    pair_window<E, R>(u1_row(P - 2 * E - B), wb[0]);  // the first main iteration's row
+    int bs = P & (K - 1);
+    for (int b = P; b <= i_last; b += P) {
+      auto body = [&](auto qc) {
+        constexpr int q = decltype(qc)::value;
+        constexpr int q2 = ((q + 1 - B) % P + P) % P;
+        constexpr int so = (q2 + E + 1) % P;
+        constexpr int cs = pf_slot<P>(q), ns = pf_slot<P>((q + 1) % P);
+        const int i = b + q;
+        if (i > i_last) return;
+        issue((bs + q + DT) & (K - 1));
+        const int m2 = i - 2 * E - B;
+        const bool bend = (i & (B - 1)) == B - 1;
+        const bool more = i + 1 <= i_last;
+        if (more && !bend) pair_window<E, R>(u1_row(m2 + 1), wb[ns]);
+        pair_scatter<E, q2>(wb[cs], acc, kc);
         if (m2 >= 2 * E) {
           const double o0 = alpha * acc[0][so];
           const double o1 = alpha * acc[1][so];
@@ -430,12 +653,15 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
             dst[xo] = o0;
           }
         }
-        block_end(i);
+        if (bend) {
+          block_end(i);
+          if (more) pair_window<E, R>(u1_row(m2 + 1), wb[ns]);
+        }
       };
       static_for<P>(body);
       bs = (bs + P) & (K - 1);
     }
-    wait_vmcnt<0>();  // drain the clamped tail DMAs and the stores
+    wait_vmcnt<0>();
   }
 }
 
@@ -635,7 +861,8 @@ template <int E>
 int pair_blocks_per_cu_e(int variant) {
   int n = 0;
   const hipError_t e =
-      variant == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_pair_mw<E, kPairMwD>, 192, 0)
+      variant == 3 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_pair_pf<E, kPairSplitD>, 128, 0)
+      : variant == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_pair_mw<E, kPairMwD>, 192, 0)
       : variant == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_pair_split<E, kPairSplitD>, 128, 0)
                      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_pair<E, kPairD>, 64, 0);
   return e == hipSuccess ? n : 0;
@@ -643,7 +870,9 @@ int pair_blocks_per_cu_e(int variant) {
 
 template <int E>
 int launch_pair_e(const RectList &rl, const StepConst &c, int variant, hipStream_t st) {
-  if (variant == 2)
+  if (variant == 3)
+    hipLaunchKernelGGL((k_pair_pf<E, kPairSplitD>), dim3(rl.nwork), dim3(128), 0, st, rl, c);
+  else if (variant == 2)
     hipLaunchKernelGGL((k_pair_mw<E, kPairMwD>), dim3(rl.nwork), dim3(192), 0, st, rl, c);
   else if (variant == 1)
     hipLaunchKernelGGL((k_pair_split<E, kPairSplitD>), dim3(rl.nwork), dim3(128), 0, st, rl, c);

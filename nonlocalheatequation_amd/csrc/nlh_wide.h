@@ -1,0 +1,319 @@
+// nlh_wide.h -- single-step production kernel for large horizons, k_wide
+// (E = 17..32; C4's eps = 32 among them).  Same operator as k_fast (reference
+// sum_local, src/2d_nonlocal_serial.cpp:256-270, J = 1; update :279-284), laid
+// out for one wave per SIMD:
+//
+//   * one column per lane (64-column strips): the 2E+C live accumulators of a
+//     column fill most of the 256 VGPRs a wave can address;
+//   * accumulators in BLOCKS of C output rows: indexed by compile-time offsets
+//     inside a chunk of C input rows and renamed (2E register moves) once per
+//     chunk, so the row loop unrolls by C = 16 rows instead of k_fast's 2E+1.
+//     At E = 32 k_fast's 65-row unroll is ~120 KB of code, about twice the
+//     instruction cache; k_wide's chunk is a fraction of that;
+//   * the window (2E+1 values per lane) streams from LDS in groups of levels,
+//     the reads of group g+1 issued before the adds of group g, so it never
+//     occupies more than a few registers;
+//   * centre fold (u' = alpha (S + (1/alpha - N) u), as k_pair): no ring of
+//     centre rows; the fast test-mode source dt*b(k) enters the accumulator of
+//     output k at its centre row as (dt/alpha)*b(k).
+//
+// Input rows stream HBM -> LDS by LDS-DMA (global_load_lds_dwordx4) D rows
+// ahead through a ring of K = pow2 >= D+1 slots, hand-counted vmcnt waits (as
+// k_fast).  Every chunk processes C rows; rows past the segment re-read the
+// last input row and only feed outputs that are never emitted.
+//
+// Indexing (sweep down; odd segments sweep up, mirrored): input row i = 0 ..
+// n_in-1 is block row Y0-E+i, output row k = 0 .. seg-1 is block row Y0+k.
+// Input i reaches outputs k = i-E-dy, dy in [-E, E], with the row window
+// H_len(|dy|).  In chunk j (inputs i = C j + c) output k sits in accumulator
+// a = k - (C j - 2E) = c + E - dy:  a = c + 2E is first touched (dy = -E,
+// assigned), a = c + E takes the centre fold, a = c receives its last term.
+// After the chunk a = 0 .. C-1 are complete (emitted), then a -> a - C.
+#pragma once
+
+#include "nlh_device.h"
+#include "nlh_kernel_common.h"
+
+namespace nlh {
+
+constexpr int kWideC = 8;    // rows per chunk (unroll; 8 measured fastest at E = 32)
+constexpr int kWideD = 6;    // input rows in flight
+constexpr int kWideLG = 4;   // window levels per LDS read group
+
+// number of row offsets dy in [-E, E] whose disk half-width len(|dy|) is L,
+// and the t-th of them (ascending)
+__host__ __device__ constexpr int wide_taps(int E, int L) {
+  int n = 0;
+  for (int dy = -E; dy <= E; ++dy)
+    if (clen(E, dy < 0 ? -dy : dy) == L) ++n;
+  return n;
+}
+__host__ __device__ constexpr int wide_tap_dy(int E, int L, int t) {
+  for (int dy = -E; dy <= E; ++dy)
+    if (clen(E, dy < 0 ? -dy : dy) == L && t-- == 0) return dy;
+  return 0;
+}
+
+// the last level < L whose row window feeds some output (0: the centre column)
+__host__ __device__ constexpr int wide_prev_used(int E, int L) {
+  for (int l = L - 1; l > 0; --l)
+    if (wide_taps(E, l) > 0) return l;
+  return 0;
+}
+
+// p[LO] + .. + p[HI] as a balanced tree (depth log2 instead of HI-LO)
+template <int LO, int HI, int N>
+__device__ __forceinline__ double tree_sum(const double (&p)[N]) {
+  if constexpr (LO == HI)
+    return p[LO];
+  else
+    return tree_sum<LO, (LO + HI) / 2>(p) + tree_sum<(LO + HI) / 2 + 1, HI>(p);
+}
+
+// ABL (diagnostics, timing only): 1 = a scheduling barrier between rows
+template <int E, int CH, bool TEST, int D = kWideD, int ABL = 0, int PIN = 1, bool AB = false>
+__global__ __launch_bounds__(64, 1) void k_wide(RectList L, StepConst C) {
+  constexpr int W = 64;                 // output columns per strip
+  constexpr int EP = (E + 1) & ~1;      // staged halo columns per side (16-B rows)
+  constexpr int RW = W + 2 * EP;        // staged doubles per ring row
+  constexpr int NCH = RW / 2;           // 16-byte chunks per row
+  // AB: every row staged twice, copy B one column later than copy A and 16
+  // bytes further in LDS (so a lane pair reading A and B hits different banks)
+  constexpr int RWS = AB ? 2 * RW + 4 : RW;  // doubles per ring slot
+  constexpr int OB = RW + 2;                 // copy B within a slot
+  constexpr int K = pow2_ceil(D + 1);   // ring slots
+  constexpr int GU = (AB ? 2 : 1) * ((NCH + 63) / 64);  // DMA instructions per u row
+  constexpr int GL = TEST ? (W / 2 + 63) / 64 : 0;  // per L_h[W0] row
+  constexpr int G = GU + GL;
+  constexpr int NA = 2 * E + CH;        // live accumulators
+  constexpr int NG = (E + kWideLG - 1) / kWideLG;  // level groups
+  static_assert(D * G + CH < 64, "vmcnt range");
+  static_assert(CH % PIN == 0, "rows per pin");
+
+  __shared__ __attribute__((aligned(16))) double ring[K * RWS + (TEST ? K * W : 0)];
+  double *lwr = ring + K * RWS;  // L_h[W0] rows (TEST), same slots as the u rows
+
+  const int lane = (int)threadIdx.x;
+  const int work = xcd_remap(blockIdx.x, gridDim.x);
+  const int ri = find_rect(L, work);
+  const Rect &Rc = L.r[ri];
+  const double *const ru = Rc.u;
+  double *const run = Rc.un;
+  const int rx1 = Rc.x1, rgx0 = Rc.gx0, rgy0 = Rc.gy0;
+  const int local = work - Rc.wg_begin;
+  const int nstrip = Rc.nstrip;
+  const int strip = local % nstrip, seg = local / nstrip;
+  const int x0 = Rc.x0 + strip * W;
+  const int seg_h = Rc.seg_rows;
+  const int Y0 = Rc.y0 + seg * seg_h;
+  const int Y1 = min(Y0 + seg_h, Rc.y1);
+  const int nout = Y1 - Y0;
+  const int n_in = nout + 2 * E;
+  const bool up = (seg & 1) != 0;
+  const int64_t pitch = Rc.pitch;
+  const int64_t stride = up ? -pitch : pitch;
+  const int yfirst = up ? (Y1 + E - 1) : (Y0 - E);
+  const double alpha = C.alpha, kc = C.kc;
+
+  const int xl = x0 + lane;  // the column of this lane
+  const bool emit = xl < rx1;
+  double sxv = 0.0;
+  if constexpr (TEST) sxv = C.sxt[rgx0 + min(xl, rx1 - 1) + E];
+
+  // AB: window start of this lane, staged column (EP - E) + lane of copy A,
+  // or of copy B one column earlier when that is odd
+  const int s_l = EP - E + lane;
+  const int lane_off = (s_l & 1) ? OB + s_l - 1 : s_l;
+  const uint32_t lring = __builtin_amdgcn_readfirstlane(lds_addr(ring));
+  const uint32_t llw = __builtin_amdgcn_readfirstlane(lds_addr(lwr));
+  // u rows: running pointer clamped at the last input row
+  const double *gnext = ru + (int64_t)yfirst * pitch + (x0 - EP);
+  // L_h[W0] row of output k = i - E (the centre row of input i), fetched with
+  // input row i into the same ring slot; rows -E .. nout+E-1 lie in the halo
+  const double *l0 = TEST ? Rc.lw + (int64_t)(up ? Y1 - 1 : Y0) * pitch + x0 : nullptr;
+  int fetched = 0;  // next input row to issue
+  auto issue = [&]() __attribute__((always_inline)) {
+    const int slot = fetched & (K - 1);
+    if constexpr (TEST) {
+      const int k = min(fetched, n_in - 1) - E;
+      dma_chunks<W / 2>(l0 + (int64_t)k * stride, llw + slot * W * 8, lane);
+    }
+    dma_chunks<NCH>(gnext, lring + slot * RWS * 8, lane);
+    if constexpr (AB) dma_chunks<NCH>(gnext + 1, lring + (slot * RWS + OB) * 8, lane);
+    ++fetched;
+    if (fetched < n_in) gnext += stride;
+  };
+#pragma unroll
+  for (int s = 0; s < D; ++s) issue();
+
+  double acc[NA];
+#pragma unroll
+  for (int a = 0; a < NA; ++a) acc[a] = 0.0;
+
+  const double qs = TEST ? C.dt / alpha : 0.0;
+  const int nchunk = (n_in + CH - 1) / CH;
+  bool full = false;  // the previous chunk stored CH output rows
+  for (int j = 0; j < nchunk; ++j) {
+    const int ibase = j * CH;
+    auto row = [&](auto cc) __attribute__((always_inline)) {
+      constexpr int c = decltype(cc)::value;
+      if constexpr ((ABL & 1) != 0) __builtin_amdgcn_sched_barrier(0);
+      const int i = ibase + c;
+      issue();  // input row i + D
+      // row i landed.  Issued after its DMA: the DMAs of rows i+1 .. i+D,
+      // and for c < D the CH output stores of the previous chunk's end
+      if constexpr (c < D) {
+        if (full)
+          wait_vmcnt<D * G + CH>();
+        else
+          wait_vmcnt<D * G>();
+      } else {
+        wait_vmcnt<D * G>();
+      }
+      // this lane's window: staged columns xl-E .. xl+E
+      // this lane's window w[0 .. 2E] (w[E] its own column).  AB: read as
+      // 16-byte pairs from copy A or B of the row, whichever has it aligned
+      // (ds_read_b128: 4 LDS cycles per KB; 8-byte reads paired by the
+      // compiler into ds_read2_b64 take 8, and LDS-bound the kernel)
+      const double *wrow = AB ? ring + (i & (K - 1)) * RWS + lane_off
+                              : ring + (i & (K - 1)) * RWS + (EP - E) + lane;
+      auto wpair = [&](int k2) __attribute__((always_inline)) {  // w[2 k2], w[2 k2 + 1]
+        return *reinterpret_cast<const double2 *>(wrow + 2 * k2);
+      };
+      double wl[NG][kWideLG], wr[NG][kWideLG];
+      auto load_group = [&](auto gc) __attribute__((always_inline)) {
+        constexpr int g = decltype(gc)::value;
+        constexpr int L0 = g * kWideLG + 1;
+        constexpr int LN = L0 + kWideLG - 1 < E ? L0 + kWideLG - 1 : E;
+        if constexpr (AB) {
+          double lv[2 * kWideLG + 2], rv[2 * kWideLG + 2];
+          constexpr int lk0 = (E - LN) / 2, lk1 = (E - L0) / 2;  // pairs covering w[E-LN .. E-L0]
+          constexpr int rk0 = (E + L0) / 2, rk1 = (E + LN) / 2;  // pairs covering w[E+L0 .. E+LN]
+#pragma unroll
+          for (int k = lk0; k <= lk1; ++k) {
+            const double2 v = wpair(k);
+            lv[2 * (k - lk0)] = v.x;
+            lv[2 * (k - lk0) + 1] = v.y;
+          }
+#pragma unroll
+          for (int k = rk0; k <= rk1; ++k) {
+            const double2 v = wpair(k);
+            rv[2 * (k - rk0)] = v.x;
+            rv[2 * (k - rk0) + 1] = v.y;
+          }
+#pragma unroll
+          for (int t = 0; t < kWideLG; ++t) {
+            if (L0 + t <= E) {
+              wl[g][t] = lv[E - (L0 + t) - 2 * lk0];
+              wr[g][t] = rv[E + (L0 + t) - 2 * rk0];
+            }
+          }
+        } else {
+#pragma unroll
+          for (int t = 0; t < kWideLG; ++t) {
+            if (L0 + t <= E) {
+              wl[g][t] = wrow[E - (L0 + t)];
+              wr[g][t] = wrow[E + (L0 + t)];
+            }
+          }
+        }
+      };
+      const double wc = AB ? ((E % 2 == 0) ? wpair(E / 2).x : wpair(E / 2).y) : wrow[E];
+      load_group(std::integral_constant<int, 0>{});
+      // dy = -E: first term of output a = c + 2E; dy = +E: last of a = c
+      acc[c + 2 * E] = wc;
+      acc[c] += wc;
+      double core = wc;
+      double pend = 0.0;  // p of levels not yet folded into core
+      auto group = [&](auto gc) __attribute__((always_inline)) {
+        constexpr int g = decltype(gc)::value;
+        // region = the next group's LDS reads + this group's adds: the
+        // scheduler may not hoist later reads (register pressure) or sink
+        // these adds past them
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (g + 1 < NG) load_group(std::integral_constant<int, g + 1>{});
+        // the window sum grows by p_L = w[E-L] + w[E+L] per level; it is only
+        // needed at levels some output uses, so the p of the levels between
+        // two used ones are summed as a tree and folded in once (the same
+        // adds as the level-by-level chain, a fraction of its depth).
+        // Levels past the group's last used one carry over in `pend`.
+        constexpr int L0 = g * kWideLG + 1;
+        double pp[kWideLG];
+#pragma unroll
+        for (int t = 0; t < kWideLG; ++t)
+          if (L0 + t <= E) pp[t] = wl[g][t] + wr[g][t];
+        auto level = [&](auto tc) __attribute__((always_inline)) {
+          constexpr int t = decltype(tc)::value;
+          constexpr int Lv = L0 + t;
+          if constexpr (Lv <= E && wide_taps(E, Lv) > 0) {
+            constexpr int s0 = wide_prev_used(E, Lv) + 1;  // first level of this segment
+            constexpr int lo = s0 > L0 ? s0 - L0 : 0;
+            const double seg = tree_sum<lo, t>(pp);
+            if constexpr (s0 < L0)  // the segment began in an earlier group
+              core = core + (pend + seg);
+            else
+              core = core + seg;
+            auto tap = [&](auto kk) __attribute__((always_inline)) {
+              constexpr int dy = wide_tap_dy(E, Lv, decltype(kk)::value);
+              acc[c + E - dy] += core;
+            };
+            static_for<wide_taps(E, Lv)>(tap);
+          }
+        };
+        static_for<kWideLG>(level);
+        // levels after the group's last used one: carried to the next group
+        constexpr int LE = L0 + kWideLG - 1 < E ? L0 + kWideLG - 1 : E;
+        constexpr int s0 = wide_prev_used(E, LE + 1) + 1;  // first unfolded level
+        if constexpr (LE < E && s0 <= LE) {
+          constexpr int lo = s0 > L0 ? s0 - L0 : 0;
+          const double seg = tree_sum<lo, LE - L0>(pp);
+          if constexpr (s0 < L0)
+            pend = pend + seg;
+          else
+            pend = seg;
+        }
+      };
+      static_for<NG>(group);
+      acc[c + E] = fma(kc, wc, acc[c + E]);
+      if constexpr (TEST) {
+        // b = -(2 pi st) W0 - ct L_h[W0] at output k = i - E
+        const int k = i - E;
+        const int y = up ? (Y1 - 1 - k) : (Y0 + k);
+        const double syv = C.syt[rgy0 + y + E];
+        const double b = -(C.st2pi * (sxv * syv)) - C.ct * lwr[(i & (K - 1)) * W + lane];
+        acc[c + E] = fma(qs, b, acc[c + E]);
+      }
+      // pin the adds of the last PIN rows before the next row's DMA / wait / LDS
+      // reads: unpinned, the compiler sinks them and keeps many rows' windows
+      // live (spills); pinned every PIN rows, PIN rows' dependency chains
+      // (the nested-window core) interleave
+      if constexpr (c % PIN == PIN - 1) {
+#pragma unroll
+        for (int a = c + 1 - PIN; a <= c + 2 * E; ++a) asm volatile("" : "+v"(acc[a]));
+      }
+    };
+    static_for<CH>(row);
+    // outputs a = 0 .. CH-1 complete: k = ibase - 2E + a
+    full = ibase - 2 * E >= 0 && ibase - 2 * E + CH <= nout;
+    auto store = [&](auto ac) __attribute__((always_inline)) {
+      constexpr int a = decltype(ac)::value;
+      const int k = ibase - 2 * E + a;
+      if (k < 0 || k >= nout) return;
+      if (emit) run[(int64_t)(up ? Y1 - 1 - k : Y0 + k) * pitch + xl] = alpha * acc[a];
+    };
+    static_for<CH>(store);
+    // rename: a -> a - CH
+#pragma unroll
+    for (int a = 0; a < 2 * E; ++a) acc[a] = acc[a + CH];
+  }
+  wait_vmcnt<0>();  // drain the clamped tail DMAs and the stores
+}
+
+template <int E, bool TEST>
+int launch_wide_e(const RectList &rl, const StepConst &c, hipStream_t st) {
+  hipLaunchKernelGGL((k_wide<E, kWideC, TEST>), dim3(rl.nwork), dim3(64), 0, st, rl, c);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : (int)e;
+}
+
+}  // namespace nlh

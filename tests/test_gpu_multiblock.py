@@ -145,7 +145,8 @@ def test_rccl_two_ranks(oracle):
 
 
 @pytest.mark.parametrize("kernel,test,eps,nt", [("exact", True, 5, 6), ("fast", False, 8, 6),
-                                                ("fast", False, 8, 5), ("fast", True, 6, 4)])
+                                                ("fast", False, 8, 5), ("fast", True, 6, 4),
+                                                ("fast", False, 20, 3), ("fast", True, 32, 2)])
 def test_rccl_self_transport(oracle, monkeypatch, kernel, test, eps, nt):
     """NLH_RCCL_SELF: one rank with a size-1 RCCL communicator; every halo
     piece between its blocks is packed, sent with ncclSend/ncclRecv to self

@@ -97,7 +97,7 @@ def test_tiled_rows_single_gpu(oracle, row):
     assert abs(l2 - l2_ref) <= 1e-10 * l2_ref
 
 
-FAST_EPS = list(range(1, 17)) + [20, 24, 32]
+FAST_EPS = list(range(1, 33))  # 1..16 k_fast / k_pair, 17..32 k_wide
 
 
 @pytest.mark.parametrize("eps", FAST_EPS)
@@ -138,13 +138,63 @@ def test_eps32_golden(kernel, test):
         assert np.max(np.abs(u - g)) <= 1e-12 * np.max(np.abs(g))
 
 
-@pytest.mark.parametrize("eps", [17, 40])
+@pytest.mark.parametrize("eps", [33, 40])
 def test_unsupported_fast_eps_falls_back_to_exact(oracle, eps):
     r = N.BatchRow(60, 50, 2, eps, 1.0, 1e-4, 1.0 / 60)
     with N.Solver(r.nx, r.ny, eps, r.k, r.dt, r.dh, test=False, kernel="auto") as s:
         assert s.info().kernel == N.KERNEL_EXACT
     with pytest.raises(N.NLHError, match="not instantiated"):
         N.Solver(r.nx, r.ny, eps, r.k, r.dt, r.dh, test=False, kernel="fast")
+
+
+@pytest.mark.parametrize("eps", [17, 22, 32])
+def test_wide_kernel_zero_alpha(oracle, eps):
+    """k_wide folds the centre term with 1/alpha: with dt = 0 (alpha = 0) AUTO
+    runs the exact kernel and an explicit FAST request is refused."""
+    with N.Solver(80, 70, eps, 1.0, 0.0, 1.0 / 80, test=False, kernel="auto") as s:
+        assert s.info().kernel == N.KERNEL_EXACT
+    with pytest.raises(N.NLHError):
+        N.Solver(80, 70, eps, 1.0, 0.0, 1.0 / 80, test=False, kernel="fast")
+
+
+@pytest.mark.parametrize("eps", [17, 20, 23, 24, 29, 32])
+@pytest.mark.parametrize("test", [False, True])
+def test_wide_kernel_vs_oracle(oracle, eps, test):
+    """k_wide (eps 17..32: one column per lane, accumulator blocks renamed per
+    8-row chunk, centre fold, fast test-mode source folded at the centre row)
+    against the oracle on ragged lattices (segments and strips partial),
+    random IC in production mode, the manufactured solution in test mode."""
+    nx, ny, nt = 197, 263, 4
+    dh = 1.0 / nx
+    dt = eps ** 4 * dh * dh / (8 * N.disk_count(eps))
+    rng = np.random.default_rng(40 + eps)
+    u0 = None if test else rng.uniform(-1.0, 1.0, size=(ny, nx))
+    r = N.BatchRow(nx, ny, nt, eps, 1.0, dt, dh)
+    u_ref, l2_ref, _ = _oracle_run(oracle, r, test, u0)
+    u, l2, _, info = _gpu_run(r, test, "auto", u0)
+    assert info.pass_kernel == "k_wide" and info.kernel == N.KERNEL_FAST
+    scale = np.max(np.abs(u_ref))
+    assert np.max(np.abs(u - u_ref)) <= 1e-12 * scale
+    if test:
+        assert abs(l2 - l2_ref) <= 1e-10 * l2_ref
+
+
+@pytest.mark.parametrize("seg", [1, 9, 64, 1000])
+def test_wide_kernel_segment_heights(oracle, seg):
+    """Segments shorter than a chunk, shorter than the horizon, and one
+    segment per strip."""
+    nx, ny, eps, nt = 150, 120, 24, 3
+    dh = 1.0 / nx
+    dt = 0.9 * eps ** 4 * dh * dh / (8 * N.disk_count(eps))
+    u0 = np.random.default_rng(seg).uniform(-1.0, 1.0, size=(ny, nx))
+    ref = oracle.run(oracle.params(nx, ny, eps, 1.0, dt, dh, 0), nt, u0)
+    with N.Solver(nx, ny, eps, 1.0, dt, dh, test=False, kernel="fast", seg_rows=seg) as s:
+        s.input_init(u0)
+        s.run(nt)
+        s.synchronize()
+        u = s.field()
+        assert s.info().pass_kernel == "k_wide"
+    assert np.max(np.abs(u - ref)) <= 1e-12 * np.max(np.abs(ref))
 
 
 @pytest.mark.parametrize("r", [1, 2, 4])
@@ -217,7 +267,7 @@ def test_pair_split_bitwise_equals_one_wave_pair(monkeypatch, eps):
     dt = 0.8 * eps ** 4 * dh * dh / (8 * N.disk_count(eps))
     u0 = rng.uniform(-1.0, 1.0, size=(ny, nx))
     out = {}
-    for split in ("1", "0", "2"):
+    for split in ("1", "0", "2", "3"):
         monkeypatch.setenv("NLH_PAIR_SPLIT", split)
         with N.Solver(nx, ny, eps, 1.0, dt, dh, test=False, kernel="fast", seg_rows=37) as s:
             s.input_init(u0)
@@ -227,6 +277,7 @@ def test_pair_split_bitwise_equals_one_wave_pair(monkeypatch, eps):
             assert s.info().steps_per_pass == 2
     assert np.array_equal(out["1"].view(np.uint64), out["0"].view(np.uint64))
     assert np.array_equal(out["2"].view(np.uint64), out["0"].view(np.uint64))
+    assert np.array_equal(out["3"].view(np.uint64), out["0"].view(np.uint64))
 
 
 @pytest.mark.parametrize("eps", [13, 15])

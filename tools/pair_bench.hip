@@ -1,0 +1,173 @@
+// pair_bench.hip -- standalone timing harness for two-step pass variants
+// (nlh_pair.h) on one C2-sized block, without rebuilding libnlh.  Each
+// variant advances the same field; results are compared bitwise with the
+// first (reference) variant after the same number of passes.
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -Iinclude -Inonlocalheatequation_amd/csrc \
+//     -mllvm -pragma-unroll-threshold=1000000 tools/pair_bench.hip -o build/pair_bench
+//   build/pair_bench [n=4096] [passes=200] [seg_rows=0: auto list]
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "nlh_pair.h"
+
+using namespace nlh;
+
+#define CK(x)                                                                      \
+  do {                                                                             \
+    hipError_t e_ = (x);                                                           \
+    if (e_ != hipSuccess) {                                                        \
+      std::fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+      std::exit(1);                                                                \
+    }                                                                              \
+  } while (0)
+
+typedef void (*KFn)(RectList, StepConst);
+
+struct Variant {
+  const char *name;
+  KFn fn;
+  int threads;
+  int wg_per_cu;  // resident workgroups per CU the segment height is sized for
+  int strip_out;  // output columns per strip
+};
+
+constexpr int E = 8;
+
+static int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+int main(int argc, char **argv) {
+  const int n = argc > 1 ? std::atoi(argv[1]) : 4096;
+  const int passes = argc > 2 ? std::atoi(argv[2]) : 200;
+  const int seg_force = argc > 3 ? std::atoi(argv[3]) : 0;
+  const int H = 2 * E, XL = 16;
+  const int64_t pitch = ((XL + std::max<int64_t>(ceil_div(n, 256) * 256 + XL, n + 128)) + 7) / 8 * 8;
+  const int64_t rows = n + 2 * H;
+  const size_t bytes = (size_t)(pitch * rows) * sizeof(double);
+  double *buf[2];
+  for (auto &b : buf) {
+    CK(hipMalloc(&b, bytes));
+    CK(hipMemset(b, 0, bytes));
+  }
+  std::vector<double> h((size_t)n * n);
+  const double dh = 1.0 / n;
+  for (int y = 0; y < n; ++y)
+    for (int x = 0; x < n; ++x) h[(size_t)y * n + x] = std::sin(2 * M_PI * (x * dh)) * std::sin(2 * M_PI * (y * dh)) +
+                                                      0.25 * std::sin(2 * M_PI * (7 * x * dh + 3 * y * dh));
+  auto origin = [&](double *b) { return b + (int64_t)H * pitch + XL; };
+  int disk = 0;
+  for (int d = -E; d <= E; ++d) disk += 2 * clen(E, d < 0 ? -d : d) + 1;
+  StepConst C{};
+  const double dt = std::pow((double)E, 4) * dh * dh / (8.0 * disk);
+  C.c2d = 8.0 / std::pow(E * dh, 4);
+  C.dh2 = dh * dh;
+  C.dt = dt;
+  C.alpha = C.c2d * C.dh2 * dt;
+  C.nf = disk;
+  C.kc = 1.0 / C.alpha - disk;
+  C.nx = n;
+  C.ny = n;
+  C.E = E;
+
+  hipDeviceProp_t prop;
+  CK(hipGetDeviceProperties(&prop, 0));
+  const int cus = prop.multiProcessorCount;
+
+  // ablation masks of k_pair_split: 2 no HBM, 4 no LDS window reads,
+  // 8 no s_barrier, 16 no u^{t+1} LDS writes
+  std::vector<Variant> vs = {
+      {"split_D8_B4", k_pair_split<E, 8, 0, 4>, 128, 4, 128 - 2 * E},
+      {"split_abl512_ntstore", k_pair_split<E, 8, 512, 4>, 128, 4, 128 - 2 * E},
+      {"split_abl1024_tDMA", k_pair_split<E, 8, 1024, 4>, 128, 4, 128 - 2 * E},
+      {"split_abl1536_ntstore_tDMA", k_pair_split<E, 8, 1536, 4>, 128, 4, 128 - 2 * E},
+      {"split_D8_B4_seg76", k_pair_split<E, 8, 0, 4>, 128, 8, 128 - 2 * E},
+      {"split_D8_B4_seg304", k_pair_split<E, 8, 0, 4>, 128, 2, 128 - 2 * E},
+  };
+
+  std::vector<double> ref((size_t)n * n), got((size_t)n * n);
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (size_t vi = 0; vi < vs.size(); ++vi) {
+    const Variant &v = vs[vi];
+    // segment height: minimise rounds x (seg + 3E) over the resident slots
+    const int nstrip = (int)ceil_div(n, v.strip_out);
+    int seg = seg_force;
+    if (!seg) {
+      int64_t best = -1, bc = 0;
+      for (int64_t k = 1; k <= 1024; ++k) {
+        const int64_t sg = std::max<int64_t>(16, ceil_div(n, k));
+        const int64_t wgs = nstrip * ceil_div(n, sg);
+        const int64_t cost = ceil_div(wgs, (int64_t)v.wg_per_cu * cus) * (sg + 3 * E);
+        if (best < 0 || cost < bc) {
+          best = sg;
+          bc = cost;
+        }
+        if (sg == 16) break;
+      }
+      seg = (int)best;
+    }
+    RectList L{};
+    L.nrects = 1;
+    Rect &R = L.r[0];
+    R.pitch = pitch;
+    R.x0 = 0;
+    R.y0 = 0;
+    R.x1 = n;
+    R.y1 = n;
+    R.gx0 = 0;
+    R.gy0 = 0;
+    R.seg_rows = seg;
+    R.nstrip = nstrip;
+    R.nseg = (int)ceil_div(n, seg);
+    R.wg_begin = 0;
+    L.nwork = R.nstrip * R.nseg;
+    C.seg_pair = seg;
+    // same initial field for every variant
+    CK(hipMemcpy2D(origin(buf[0]), pitch * 8, h.data(), (size_t)n * 8, (size_t)n * 8, n, hipMemcpyHostToDevice));
+    int cur = 0;
+    auto launch = [&](int k) {
+      R.u = origin(buf[cur]);
+      R.un = origin(buf[1 - cur]);
+      for (int j = 0; j < k; ++j) {
+        L.r[0].u = origin(buf[cur]);
+        L.r[0].un = origin(buf[1 - cur]);
+        hipLaunchKernelGGL(v.fn, dim3(L.nwork), dim3(v.threads), 0, 0, L, C);
+        cur = 1 - cur;
+      }
+    };
+    launch(4);  // check pass count: identical for every variant
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy2D(got.data(), (size_t)n * 8, origin(buf[cur]), pitch * 8, (size_t)n * 8, n, hipMemcpyDeviceToHost));
+    bool same = true;
+    double maxd = 0;
+    if (vi == 0) {
+      ref = got;
+    } else {
+      same = std::memcmp(ref.data(), got.data(), ref.size() * 8) == 0;
+      for (size_t i = 0; i < ref.size(); ++i) maxd = std::max(maxd, std::fabs(ref[i] - got[i]));
+    }
+    launch(20);
+    float best_ms = 1e30f;
+    for (int r = 0; r < 3; ++r) {
+      CK(hipEventRecord(e0, 0));
+      launch(passes);
+      CK(hipEventRecord(e1, 0));
+      CK(hipEventSynchronize(e1));
+      float ms = 0;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      best_ms = std::min(best_ms, ms);
+    }
+    const double us = best_ms * 1e3 / passes;
+    std::printf("{\"variant\": \"%s\", \"n\": %d, \"seg\": %d, \"wgs\": %d, \"us_per_pass\": %.2f, "
+                "\"us_per_step\": %.2f, \"gnode_s\": %.1f, \"bitwise_vs_first\": %s, \"maxdiff\": %.3g}\n",
+                v.name, n, seg, L.nwork, us, us / 2, 2.0 * n * n / us / 1e3, same ? "true" : "false", maxd);
+    std::fflush(stdout);
+  }
+  return 0;
+}
