@@ -112,8 +112,8 @@ __device__ __forceinline__ void pair_scatter(const double (&w)[2 * E + 2], doubl
 // also: 4 = windows from registers (no LDS window reads), 8 = no s_barrier,
 // 16 = no u^{t+1} LDS writes, 32 = no per-row range checks (rows past the
 // segment end computed too), 64 = no vmcnt waits for the DMA'd rows, 128 = no
-// output stores, 256 = no DMA, 512 = non-temporal stores, 1024 = temporal
-// (non-nt) DMA (timing decompositions; results meaningless except 512/1024)
+// output stores, 256 = no DMA, 512 = non-temporal stores, 1024 = non-temporal
+// DMA (timing decompositions; results meaningless except 512/1024)
 template <int E, int D, int ABL = 0>
 __global__ __launch_bounds__(64, (E <= 9 ? 2 : 1)) void k_pair(RectList L, StepConst C) {
   constexpr int R = 2;
@@ -397,10 +397,13 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
     const uint32_t lring = __builtin_amdgcn_readfirstlane(lds_addr(ring));
     int row = 0;  // next u^t row to fetch (clamped at the last one)
     auto issue = [&](int slot) {
-      if constexpr ((ABL & 1024) != 0)  // ablation: temporal (non-nt) DMA
-        dma_chunks<NCH, false, false>(gnext, lring + slot * RW * 8, lane);
-      else if (!(ABL & 2) && !(ABL & 256))
+      // default-policy (temporal) DMA: a strip's 2E halo columns are read
+      // again by its neighbours on the same XCD (L2 hits); nt loads measured
+      // 1-3% slower here (profiles/r02/pair_bench_5.jsonl); ABL 1024 = nt
+      if constexpr ((ABL & 1024) != 0)
         dma_chunks<NCH>(gnext, lring + slot * RW * 8, lane);
+      else if (!(ABL & 2) && !(ABL & 256))
+        dma_chunks<NCH, false, false>(gnext, lring + slot * RW * 8, lane);
       if constexpr ((ABL & 32) != 0)
         gnext += stride;
       else if (++row < n_in)

@@ -1,37 +1,46 @@
 #!/usr/bin/env python3
-"""Summarise tools/pmc.sh output for one kernel (default: the fast stencil).
+"""Summarise tools/pmc.sh output for one kernel into the record bench.py reads
+as roofline.physical (profiles/pmc/<kernel>__<workload>.json).
 
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch (rocprofv3 derived metrics).
 gfx950 correction (MI355X_MICROARCH.md 'HBM'): FETCH_SIZE reports exactly half
 the bytes of wide coalesced streaming reads -> doubled here; WRITE_SIZE is
-exact for 16-B-per-lane stores.  Usage:
-    python tools/pmc_summary.py gpurun_out/pmc1 [kernel-substring] > summary.json
+exact for 16-B-per-lane stores.  SQ_* are per dispatch, summed over the chip.
+
+    python tools/pmc_summary.py DIR KERNEL [--workload KEY --node-updates N --commit SHA]
+
+KERNEL is the short kernel name (k_pair_split, k_wide, k_fast, k_exact); it
+is matched against rocprofv3's demangled names as "KERNEL<".
 """
+import argparse
 import csv
 import glob
 import json
 import os
 import statistics
-import sys
 
 
 def main():
-    d = sys.argv[1]
-    key = sys.argv[2] if len(sys.argv) > 2 else "k_fast"
-    vals = {}
-    durs = []
-    for f in sorted(glob.glob(os.path.join(d, "p*", "run_counter_collection.csv"))):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir")
+    ap.add_argument("kernel")
+    ap.add_argument("--workload", default=None)
+    ap.add_argument("--node-updates", type=float, default=None, help="node-updates per launch")
+    ap.add_argument("--commit", default=None)
+    a = ap.parse_args()
+    key = a.kernel + "<"
+    vals, durs = {}, []
+    for f in sorted(glob.glob(os.path.join(a.dir, "p*", "run_counter_collection.csv"))):
         for row in csv.DictReader(open(f)):
-            if key not in row["Kernel_Name"]:
-                continue
-            vals.setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
-    for f in sorted(glob.glob(os.path.join(d, "p*", "run_kernel_trace.csv"))):
+            if key in row["Kernel_Name"]:
+                vals.setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
+    for f in sorted(glob.glob(os.path.join(a.dir, "p*", "run_kernel_trace.csv"))):
         for row in csv.DictReader(open(f)):
             if key in row["Kernel_Name"]:
                 durs.append(int(row["End_Timestamp"]) - int(row["Start_Timestamp"]))
     med = {k: statistics.median(v) for k, v in vals.items()}
-    out = {"kernel_match": key, "dispatches_per_counter": {k: len(v) for k, v in vals.items()},
-           "median": med}
+    out = {"kernel_match": a.kernel, "workload": a.workload, "commit": a.commit,
+           "dispatches_per_counter": {k: len(v) for k, v in vals.items()}, "median": med}
     if "FETCH_SIZE" in med and "WRITE_SIZE" in med:
         rd = 2.0 * med["FETCH_SIZE"] * 1024
         wr = med["WRITE_SIZE"] * 1024
@@ -39,6 +48,14 @@ def main():
         out["hbm_write_bytes_per_launch"] = wr
         out["hbm_bytes_per_launch"] = rd + wr
         out["correction"] = "FETCH_SIZE x2 (gfx950 half-count of wide streaming reads), KiB -> bytes"
+    if "SQ_INSTS_VALU" in med:
+        out["valu_insts_per_launch"] = med["SQ_INSTS_VALU"]
+    if a.node_updates:
+        out["node_updates_per_launch"] = a.node_updates
+        if "hbm_bytes_per_launch" in out:
+            out["hbm_bytes_per_node_update"] = out["hbm_bytes_per_launch"] / a.node_updates
+        if "valu_insts_per_launch" in out:
+            out["valu_lane_ops_per_node_update"] = 64.0 * out["valu_insts_per_launch"] / a.node_updates
     if durs:
         out["profiled_duration_us_median"] = statistics.median(durs) / 1e3
     w = med.get("SQ_WAVE_CYCLES")
@@ -51,6 +68,9 @@ def main():
         out["l2_hit_rate"] = med["TCC_HIT_sum"] / max(1.0, med["TCC_HIT_sum"] + med["TCC_MISS_sum"])
     if "GRBM_GUI_ACTIVE" in med and durs:
         out["effective_clock_ghz"] = med["GRBM_GUI_ACTIVE"] / 8 / (statistics.median(durs))
+        if "SQ_LDS_IDX_ACTIVE" in med:
+            # LDS-array busy share: cycles summed over the 256 CUs
+            out["lds_busy_share"] = med["SQ_LDS_IDX_ACTIVE"] / 256 / (med["GRBM_GUI_ACTIVE"] / 8)
     print(json.dumps(out, indent=1))
 
 

@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
-"""Minimal C2 stepping program for rocprofv3 --pmc passes (no CPU baseline,
-no torch): 4096^2, eps=8, fast kernel, 10 warm-up + N timed steps."""
+"""Minimal stepping program for rocprofv3 passes (no CPU baseline, no torch):
+the bench.py workload selected by environment variables --
+NLH_N (lattice edge, 4096), NLH_EPS (8), NLH_TEST (0/1), NLH_KERNEL (fast),
+NLH_STEPS (20 timed after 10 warm-up), NLH_SEG (0 = automatic)."""
 import os
 import sys
 
@@ -12,12 +14,14 @@ n = int(os.environ.get("NLH_N", "4096"))
 eps = int(os.environ.get("NLH_EPS", "8"))
 steps = int(os.environ.get("NLH_STEPS", "20"))
 kernel = os.environ.get("NLH_KERNEL", "fast")
+test = os.environ.get("NLH_TEST", "0") == "1"
 dh = 1.0 / n
 dt = eps ** 4 * dh * dh / (8 * N.disk_count(eps))
-s = N.Solver(n, n, eps, 1.0, dt, dh, test=False, kernel=kernel, device=0,
+s = N.Solver(n, n, eps, 1.0, dt, dh, test=test, kernel=kernel, device=0,
              seg_rows=int(os.environ.get("NLH_SEG", "0")))
 s.test_init()
 s.run(10 + steps)
 s.synchronize()
+info = s.info()
 s.close()
-print("ok")
+print(f"ok {info.pass_kernel} steps_per_pass={info.steps_per_pass}")
