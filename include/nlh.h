@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define NLH_ABI_VERSION 4
+#define NLH_ABI_VERSION 5
 
 enum nlh_status {
   NLH_OK = 0,
@@ -53,8 +53,12 @@ enum nlh_status {
   NLH_ERR_UNSUPPORTED = 5  /* configuration not supported               */
 };
 
+/* Influence functions (nlh_params.influence) */
+enum nlh_influence { NLH_INFLUENCE_CONSTANT = 0, NLH_INFLUENCE_LINEAR = 1 };
+
 /* Stencil implementation.  EXACT reproduces the reference's per-term
- * floating-point order bit for bit (4 ops per neighbour).  FAST computes the
+ * floating-point order bit for bit (4 ops per neighbour; ((J c)(u_j - u_i))
+ * dh^2 with J from a per-offset table when J != 1).  FAST computes the
  * same J=1 disk sum by nested row windows (~4*eps adds per node) and, in test
  * mode, the manufactured source from a precomputed L_h[W0] field; it differs
  * from the reference only by summation rounding (<= 1e-12 of field scale per
@@ -74,7 +78,11 @@ typedef struct nlh_params {
   int32_t seg_rows;     /* FAST kernel segment height, 0 = automatic           */
   int32_t split_tiles;  /* 1: one device block per tile (no merging of a rank's */
                         /*   tiles into rectangles; exercises the halo path)  */
-  int32_t reserved_;    /* must be 0                                           */
+  int32_t influence;    /* influence function J(r), r = |y-x|/eps:            */
+                        /*   0 = J = 1 (the reference's influence_function,   */
+                        /*   src/2d_nonlocal_serial.cpp:201), 1 = J = 1 - r   */
+                        /*   (description/problem_description.tex:159); c =  */
+                        /*   2k/(M3 (eps dh)^4), pi omitted as the code :76   */
   int64_t tiles_x;      /* tile grid over the lattice (reference npx / np);    */
   int64_t tiles_y;      /*   must divide nx / ny.  1x1 for the serial driver   */
   const int32_t *owner; /* tiles_x*tiles_y owner ranks, index gx + gy*tiles_x; */

@@ -26,13 +26,16 @@ from dataclasses import dataclass
 import numpy as np
 
 __all__ = [
-    "KERNEL_AUTO", "KERNEL_EXACT", "KERNEL_FAST", "NLHError", "Solver",
+    "KERNEL_AUTO", "KERNEL_EXACT", "KERNEL_FAST", "INFLUENCE_CONSTANT", "INFLUENCE_LINEAR", "NLHError", "Solver",
     "lib", "lib_path", "comm_unique_id", "resolve_owner", "halo_plan", "block_plan",
     "disk_count", "batch_tester", "BatchRow",
 ]
 
 KERNEL_AUTO, KERNEL_EXACT, KERNEL_FAST = 0, 1, 2
 _KERNEL_NAMES = {"auto": KERNEL_AUTO, "exact": KERNEL_EXACT, "fast": KERNEL_FAST}
+# influence function J(r), r = |y - x| / eps (nlh_params.influence)
+INFLUENCE_CONSTANT, INFLUENCE_LINEAR = 0, 1
+_INFLUENCE_NAMES = {"constant": INFLUENCE_CONSTANT, "linear": INFLUENCE_LINEAR}
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 
@@ -51,7 +54,7 @@ class _Params(ctypes.Structure):
         ("k", ctypes.c_double), ("dt", ctypes.c_double), ("dh", ctypes.c_double),
         ("test", ctypes.c_int32), ("kernel", ctypes.c_int32), ("device", ctypes.c_int32),
         ("rank", ctypes.c_int32), ("nranks", ctypes.c_int32), ("seg_rows", ctypes.c_int32),
-        ("split_tiles", ctypes.c_int32), ("reserved_", ctypes.c_int32),
+        ("split_tiles", ctypes.c_int32), ("influence", ctypes.c_int32),
         ("tiles_x", ctypes.c_int64), ("tiles_y", ctypes.c_int64),
         ("owner", ctypes.POINTER(ctypes.c_int32)),
         ("comm_id", ctypes.POINTER(ctypes.c_uint8)),
@@ -147,7 +150,7 @@ def resolve_owner(tiles_x: int, tiles_y: int, nranks: int, owner=None) -> np.nda
 
 
 def _make_params(nx, ny, eps, k, dt, dh, test, kernel, device, rank, nranks, seg_rows,
-                 tiles, owner, comm_id, split_tiles=False):
+                 tiles, owner, comm_id, split_tiles=False, influence=0):
     p = _Params()
     p.nx, p.ny, p.eps = int(nx), int(ny), int(eps)
     p.k, p.dt, p.dh = float(k), float(dt), float(dh)
@@ -156,6 +159,7 @@ def _make_params(nx, ny, eps, k, dt, dh, test, kernel, device, rank, nranks, seg
     p.device, p.rank, p.nranks, p.seg_rows = int(device), int(rank), int(nranks), int(seg_rows)
     p.tiles_x, p.tiles_y = int(tiles[0]), int(tiles[1])
     p.split_tiles = int(bool(split_tiles))
+    p.influence = _INFLUENCE_NAMES[influence] if isinstance(influence, str) else int(influence)
     keep = []
     if owner is not None:
         o = np.ascontiguousarray(owner, dtype=np.int32)
@@ -239,14 +243,14 @@ class Solver:
 
     def __init__(self, nx, ny, eps, k=1.0, dt=0.0005, dh=0.02, *, test=False, kernel="auto",
                  device=-1, rank=0, nranks=1, tiles=(1, 1), owner=None, comm_id=None, seg_rows=0,
-                 split_tiles=False):
+                 split_tiles=False, influence="constant"):
         self.nx, self.ny, self.eps = int(nx), int(ny), int(eps)
         self.k, self.dt, self.dh = float(k), float(dt), float(dh)
         self.test = bool(test)
         self.error_l2 = 0.0
         self.error_linf = 0.0
         p, keep = _make_params(nx, ny, eps, k, dt, dh, test, kernel, device, rank, nranks,
-                               seg_rows, tiles, owner, comm_id, split_tiles)
+                               seg_rows, tiles, owner, comm_id, split_tiles, influence)
         h = ctypes.c_void_p()
         _check(lib().nlh_create(ctypes.byref(p), ctypes.byref(h)), "nlh_create")
         del keep

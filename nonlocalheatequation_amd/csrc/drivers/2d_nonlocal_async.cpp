@@ -19,6 +19,8 @@
 
 using namespace nlh_drv;
 
+static int g_influence = NLH_INFLUENCE_CONSTANT;  // --influence (extra flag)
+
 static int solve(int64_t nx, int64_t ny, int64_t np, int64_t nt, int64_t eps, double k, double dt,
                  double dh, bool test, int64_t nlog, int kernel, int device, nlh_solver **out,
                  uint64_t &elapsed) {
@@ -31,6 +33,7 @@ static int solve(int64_t nx, int64_t ny, int64_t np, int64_t nt, int64_t eps, do
   p.dh = dh;
   p.test = test;
   p.kernel = kernel;
+  p.influence = g_influence;
   p.device = device;
   p.rank = 0;
   p.nranks = 1;
@@ -65,6 +68,7 @@ int main(int argc, char **argv) {
   o.opt("dh", "0.02");
   o.flag("no-header");
   o.opt("kernel", "auto");
+  o.opt("influence", "constant");
   o.opt("device", "-1");
   std::string err;
   if (!o.parse(argc, argv, err)) {
@@ -73,6 +77,11 @@ int main(int argc, char **argv) {
   }
   const bool header = !o.count("no-header");
   const int kernel = kernel_from_name(o.str("kernel"));
+  g_influence = influence_from_name(o.str("influence"));
+  if (g_influence < 0) {
+    std::cerr << "--influence must be constant or linear" << std::endl;
+    return 1;
+  }
   const int device = (int)o.as_i64("device");
   const int64_t nlog = (int64_t)o.as_u64("nlog");
 

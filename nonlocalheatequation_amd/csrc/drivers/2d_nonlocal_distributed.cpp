@@ -23,6 +23,8 @@
 
 using namespace nlh_drv;
 
+static int g_influence = NLH_INFLUENCE_CONSTANT;  // --influence (extra flag)
+
 struct Run {
   int64_t nx, ny, npx, npy, nt, eps;
   double k, dt, dh;
@@ -41,6 +43,7 @@ static int make_solver(const Run &r, const RankEnv &re, const uint8_t *id, int k
   p.dh = r.dh;
   p.test = r.test;
   p.kernel = kernel;
+  p.influence = g_influence;
   p.device = device >= 0 ? device : re.local_rank;
   p.rank = re.rank;
   p.nranks = re.nranks;
@@ -79,6 +82,7 @@ int main(int argc, char **argv) {
   o.opt("dh", "0.05");
   o.flag("no-header");
   o.opt("kernel", "auto");
+  o.opt("influence", "constant");
   o.opt("device", "-1");
   std::string err;
   if (!o.parse(argc, argv, err)) {
@@ -87,6 +91,11 @@ int main(int argc, char **argv) {
   }
   const bool header = !o.count("no-header");
   const int kernel = kernel_from_name(o.str("kernel"));
+  g_influence = influence_from_name(o.str("influence"));
+  if (g_influence < 0) {
+    std::cerr << "--influence must be constant or linear" << std::endl;
+    return 1;
+  }
   const int device = (int)o.as_i64("device");
   const int64_t nlog = (int64_t)o.as_u64("nlog");
 

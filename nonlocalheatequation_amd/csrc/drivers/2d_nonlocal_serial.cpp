@@ -17,6 +17,8 @@
 
 using namespace nlh_drv;
 
+static int g_influence = NLH_INFLUENCE_CONSTANT;  // --influence (extra flag)
+
 static nlh_params make_params(int64_t nx, int64_t ny, int64_t eps, double k, double dt, double dh,
                               bool test, int kernel, int device) {
   nlh_params p{};
@@ -28,6 +30,7 @@ static nlh_params make_params(int64_t nx, int64_t ny, int64_t eps, double k, dou
   p.dh = dh;
   p.test = test;
   p.kernel = kernel;
+  p.influence = g_influence;
   p.device = device;
   p.rank = 0;
   p.nranks = 1;
@@ -82,6 +85,7 @@ int main(int argc, char **argv) {
   o.opt("dh", "0.02");
   o.flag("no-header");
   o.opt("kernel", "auto");
+  o.opt("influence", "constant");
   o.opt("device", "-1");
   std::string err;
   if (!o.parse(argc, argv, err)) {
@@ -93,6 +97,11 @@ int main(int argc, char **argv) {
   const double k = o.as_double("k"), dt = o.as_double("dt"), dh = o.as_double("dh");
   const bool header = !o.count("no-header");
   const int kernel = kernel_from_name(o.str("kernel"));
+  g_influence = influence_from_name(o.str("influence"));
+  if (g_influence < 0) {
+    std::cerr << "--influence must be constant or linear" << std::endl;
+    return 1;
+  }
   const int device = (int)o.as_i64("device");
 
   if (o.count("test_batch")) return batch_tester((int64_t)nlog, kernel, device);

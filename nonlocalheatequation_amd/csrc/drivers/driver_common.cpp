@@ -227,6 +227,12 @@ bool share_comm_id(const RankEnv &re, uint8_t id[NLH_COMM_ID_BYTES], std::string
   return ok;
 }
 
+int influence_from_name(const std::string &s) {
+  if (s == "constant") return NLH_INFLUENCE_CONSTANT;
+  if (s == "linear") return NLH_INFLUENCE_LINEAR;
+  return -1;
+}
+
 int kernel_from_name(const std::string &s) {
   if (s == "exact") return NLH_KERNEL_EXACT;
   if (s == "fast") return NLH_KERNEL_FAST;

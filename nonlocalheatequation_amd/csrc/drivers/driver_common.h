@@ -59,6 +59,8 @@ RankEnv rank_env();
 bool share_comm_id(const RankEnv &re, uint8_t id[NLH_COMM_ID_BYTES], std::string &err);
 
 int kernel_from_name(const std::string &s);
+// --influence constant|linear -> enum nlh_influence (-1 if unknown)
+int influence_from_name(const std::string &s);
 
 // host w(x, y, t) exactly as the reference (src/2d_nonlocal_serial.cpp:207-210)
 double w_exact(int64_t x, int64_t y, int64_t t, double dt, double dh);

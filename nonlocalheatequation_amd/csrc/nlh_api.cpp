@@ -64,6 +64,7 @@ struct Resolved {
   int kernel = NLH_KERNEL_EXACT;
   bool pair = false;  // two steps per pass (nlh_pair.h)
   bool wide = false;  // large-horizon single-step kernel (nlh_wide.h)
+  bool weighted = false;  // non-constant J: k_weighted (fast) instead of the J = 1 kernels
   int halo = 0;       // eps, or 2*eps with pair
   int ablate = 0;     // diagnostics only (NLH_ABLATE)
 };
@@ -71,6 +72,19 @@ struct Resolved {
 int resolve_config(const nlh_params &p, Resolved &r) {
   const int E = (int)p.eps;
   int kern = p.kernel;
+  if (p.influence != NLH_INFLUENCE_CONSTANT && p.influence != NLH_INFLUENCE_LINEAR)
+    return fail(NLH_ERR_ARG, "influence must be NLH_INFLUENCE_CONSTANT or NLH_INFLUENCE_LINEAR");
+  if (p.influence != NLH_INFLUENCE_CONSTANT) {
+    // a non-constant J has no nested-window form: k_weighted (fast) or
+    // k_exact with the per-point J table
+    if (kern == NLH_KERNEL_AUTO) kern = nlh::weighted_supported(E) ? NLH_KERNEL_FAST : NLH_KERNEL_EXACT;
+    if (kern == NLH_KERNEL_FAST && !nlh::weighted_supported(E))
+      return fail(NLH_ERR_UNSUPPORTED, "fast weighted kernel not instantiated for eps=" + std::to_string(E));
+    r.kernel = kern;
+    r.weighted = kern == NLH_KERNEL_FAST;
+    r.halo = E;
+    return NLH_OK;
+  }
   // AUTO: the fast kernels in production AND test mode (the manufactured
   // source in its precomputed L_h[W0] form, within 1e-12 of field scale and
   // L2 within 1e-10 of the reference; EXACT remains selectable for bitwise
@@ -142,6 +156,8 @@ struct nlh_solver {
   int fast_r = 2;  // columns per lane of the fast kernel (NLH_FAST_R=1|2|4: 64/128/256-column strips)
   bool pair = false;  // two steps per pass (nlh_pair.h); production fast mode (NLH_PAIR=0 disables)
   bool wide = false;  // k_wide (nlh_wide.h) for eps 17..32
+  bool weighted = false;  // k_weighted: non-constant influence function
+  double *d_wt = nullptr, *d_qj = nullptr;  // J tables (influence != 0)
   int halo = 0;       // halo rows/columns held per block: eps, or 2*eps with pair
   int ablate = 0;     // diagnostics only (NLH_ABLATE), never set in production
   int pair_ablate = 0;  // diagnostics only (NLH_PAIR_ABLATE)
@@ -244,7 +260,8 @@ std::vector<LRect> split_block(const LocalBlock &b, int E, int sw) {
 // kind 0: single-step kernels (k_exact / k_fast); kind 1: the pair kernel
 int build_rectlists(nlh_solver *s, int kind) {
   const int E = (int)s->p.eps;
-  const bool fast = s->kernel == NLH_KERNEL_FAST;
+  // k_weighted tiles like k_exact (64-column strips, fixed segments)
+  const bool fast = s->kernel == NLH_KERNEL_FAST && !s->weighted;
   const bool pair = kind == 1;
   const int sw = pair ? nlh::pair_strip_width(E) : fast ? nlh::fast_strip_width(E, s->fast_r) : 64;
   // gather local rects (bands are s->halo wide: what the halo exchange refreshes)
@@ -342,8 +359,9 @@ int build_rectlists(nlh_solver *s, int kind) {
         R.nstrip = (int)ceil_div(R.x1 - R.x0, sw);
         R.nseg = (int)ceil_div(R.y1 - R.y0, R.seg_rows);
       } else {
+        R.seg_rows = s->weighted ? 16 : 4;
         R.nstrip = (int)ceil_div(R.x1 - R.x0, 64);
-        R.nseg = (int)ceil_div(R.y1 - R.y0, 4);
+        R.nseg = (int)ceil_div(R.y1 - R.y0, R.seg_rows);
       }
       R.wg_begin = w;
       w += R.nstrip * R.nseg;
@@ -473,7 +491,9 @@ int launch_stencil(nlh_solver *s, const std::vector<nlh::RectList> &v, hipStream
   for (const auto &rl : v) {
     if (rl.nwork == 0) continue;
     int rc;
-    if (s->wide)
+    if (s->weighted)
+      rc = nlh::launch_weighted(rl, s->sc, test, st);
+    else if (s->wide)
       rc = nlh::launch_wide(rl, s->sc, test, st);
     else if (s->kernel == NLH_KERNEL_FAST && !test && s->ablate)
       rc = nlh::launch_fast_ablation(rl, s->sc, s->ablate, st);
@@ -642,6 +662,8 @@ int destroy_impl(nlh_solver *s) {
     (void)hipFree(pr.send);
     (void)hipFree(pr.recv);
   }
+  (void)hipFree(s->d_wt);
+  (void)hipFree(s->d_qj);
   (void)hipFree(s->d_sxt);
   (void)hipFree(s->d_syt);
   (void)hipFree(s->d_lens);
@@ -712,6 +734,7 @@ int create_impl(const nlh_params *pin, nlh_solver *s) {
   s->ablate = rv.ablate;
   s->pair = rv.pair;
   s->wide = rv.wide;
+  s->weighted = rv.weighted;
   if (const char *pa = std::getenv("NLH_PAIR_ABLATE")) s->pair_ablate = std::atoi(pa);
   if (const char *fb = std::getenv("NLH_FORCE_BANDS")) s->force_bands = std::atoi(fb) != 0;
   if (const char *rs = std::getenv("NLH_RCCL_SELF")) s->rccl_self = p.nranks == 1 && std::atoi(rs) != 0;
@@ -760,7 +783,34 @@ int create_impl(const nlh_params *pin, nlh_solver *s) {
   HIP_TRY(hipMemcpy(s->d_sxt, sxt.data(), sxt.size() * sizeof(double), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(s->d_syt, syt.data(), syt.size() * sizeof(double), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(s->d_lens, lens.data(), lens.size() * sizeof(int32_t), hipMemcpyHostToDevice));
-  s->sc.c2d = (p.k * 8) / pow(p.eps * p.dh, 4);
+  // c = 2k/(M3 (eps dh)^4) with the code's pi omitted (:76): J = 1 has
+  // 2/M3 = 8, the reference's (k*8); J = 1 - r has M3 = 1/20 (tex :159)
+  s->sc.c2d = p.influence == NLH_INFLUENCE_LINEAR ? (p.k * 40) / pow(p.eps * p.dh, 4)
+                                                  : (p.k * 8) / pow(p.eps * p.dh, 4);
+  s->sc.influence = p.influence;
+  if (p.influence != NLH_INFLUENCE_CONSTANT) {
+    // J(distance/eps), distance = sqrt(dx^2+dy^2) as the reference's
+    // distance() (:224-227); wt in the reference's loop order
+    auto J = [&](long dx, long dy) { return 1.0 - sqrt((double)(dx * dx + dy * dy)) / (double)p.eps; };
+    std::vector<double> wt, qj((size_t)(E + 1) * (E + 1), 0.0);
+    double jsum = 0.0;
+    for (long dx = -E; dx <= E; ++dx) {
+      const long len = lens[dx < 0 ? -dx : dx];
+      for (long dy = -len; dy <= len; ++dy) {
+        wt.push_back(J(dx, dy) * s->sc.c2d);
+        jsum += J(dx, dy);
+      }
+    }
+    for (long dx = 0; dx <= E; ++dx)
+      for (long dy = 0; dy <= lens[dx]; ++dy) qj[(size_t)(dx * (E + 1) + dy)] = J(dx, dy);
+    HIP_TRY(hipMalloc(&s->d_wt, wt.size() * sizeof(double)));
+    HIP_TRY(hipMalloc(&s->d_qj, qj.size() * sizeof(double)));
+    HIP_TRY(hipMemcpy(s->d_wt, wt.data(), wt.size() * sizeof(double), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(s->d_qj, qj.data(), qj.size() * sizeof(double), hipMemcpyHostToDevice));
+    s->sc.wt = s->d_wt;
+    s->sc.qj = s->d_qj;
+    s->sc.jsum = jsum;
+  }
   s->sc.dh2 = p.dh * p.dh;
   s->sc.dt = p.dt;
   s->sc.alpha = s->sc.c2d * s->sc.dh2 * p.dt;
@@ -1143,7 +1193,8 @@ int nlh_get_info(const nlh_solver *s, nlh_info *info) {
   info->steps_per_pass = s->pair ? 2 : 1;
   const char *pk = s->pair ? (s->pair_split == 3 ? "k_pair_pf" : s->pair_split == 2 ? "k_pair_mw"
                               : s->pair_split == 1 ? "k_pair_split" : "k_pair")
-                           : s->wide ? "k_wide" : (s->kernel == NLH_KERNEL_FAST ? "k_fast" : "k_exact");
+                           : s->wide ? "k_wide" : s->weighted ? "k_weighted"
+                           : (s->kernel == NLH_KERNEL_FAST ? "k_fast" : "k_exact");
   std::snprintf(info->pass_kernel, sizeof(info->pass_kernel), "%s", pk);
   std::snprintf(info->arch, sizeof(info->arch), "%s", s->arch);
   return NLH_OK;

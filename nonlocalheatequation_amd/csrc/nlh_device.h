@@ -55,7 +55,13 @@ struct StepConst {
   int32_t seg_h;   // fast kernel segment height
   double kc;       // 1/alpha - N  (centre fold: pair and wide kernels)
   int32_t seg_pair;  // pair kernel segment height
-  int32_t pad_;
+  int32_t influence;  // nlh_influence: 0 = J = 1, else J from the tables below
+  // J != 1: wt[n] = J*c2d per disk point in the reference's loop order (sx
+  // outer, sy inner; k_exact), qj[dx*(E+1)+dy] = J(dx, dy) for the quadrant
+  // 0 <= dy <= len(dx) (k_weighted), jsum = sum of J over the disk
+  const double *wt;
+  const double *qj;
+  double jsum;
 };
 
 // Strided rectangle copy (halo exchange: local block->block copies, pack to
@@ -102,6 +108,11 @@ int launch_pair_ablation(const RectList &rl, const StepConst &c, int abl, void *
 // diagnostics (NLH_ABLATE=1|2, eps=8 only): see k_fast's ABL parameter
 int launch_fast_ablation(const RectList &rl, const StepConst &c, int abl, void *stream);
 int launch_exact(const RectList &rl, const StepConst &c, bool test, void *stream);
+// fast path for a non-constant J (influence != 0, eps <= 32): LDS tile of
+// 64 x 16 outputs per workgroup, direct weighted sum over the disk's 4-fold
+// symmetric groups; rect lists as k_exact with 16-row segments
+bool weighted_supported(int E);
+int launch_weighted(const RectList &rl, const StepConst &c, bool test, void *stream);
 // A = sum_local(u) only (no time update) -- used once for L_h[W0].
 int launch_exact_sum(const RectList &rl, const StepConst &c, void *stream);
 int launch_copies(const CopyList &cl, void *stream);

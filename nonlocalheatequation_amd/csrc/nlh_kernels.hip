@@ -40,7 +40,7 @@ namespace nlh {
 
 // ----------------------------------------------------------------------------
 // k_exact: bit-parity kernel.  64x4 nodes per 256-thread workgroup.
-template <bool TEST, bool SUMONLY>
+template <bool TEST, bool SUMONLY, bool WT>
 __global__ __launch_bounds__(256) void k_exact(RectList L, StepConst C) {
 #pragma clang fp contract(off)
   const int work = xcd_remap(blockIdx.x, gridDim.x);
@@ -56,12 +56,24 @@ __global__ __launch_bounds__(256) void k_exact(RectList L, StepConst C) {
   const double *u = R.u + (int64_t)y * p + x;
   const double ui = *u;
   double res = 0.0;
-  // sum_local (:256-270): sx outer, sy inner; out-of-domain halo cells are 0
-  for (int dx = -E; dx <= E; ++dx) {
-    const int len = C.lens[dx < 0 ? -dx : dx];
-    const double *col = u + dx;
-    for (int dy = -len; dy <= len; ++dy)
-      res += ((C.c2d * (col[(int64_t)dy * p] - ui)) * C.dh2);
+  // sum_local (:256-270): sx outer, sy inner; out-of-domain halo cells are 0.
+  // The reference's term is ((J*c)*(u_j-u_i))*(dh*dh) with J = 1.0 (:201);
+  // WT: J*c per disk point from the host table, same order
+  if constexpr (WT) {
+    int n = 0;
+    for (int dx = -E; dx <= E; ++dx) {
+      const int len = C.lens[dx < 0 ? -dx : dx];
+      const double *col = u + dx;
+      for (int dy = -len; dy <= len; ++dy, ++n)
+        res += ((C.wt[n] * (col[(int64_t)dy * p] - ui)) * C.dh2);
+    }
+  } else {
+    for (int dx = -E; dx <= E; ++dx) {
+      const int len = C.lens[dx < 0 ? -dx : dx];
+      const double *col = u + dx;
+      for (int dy = -len; dy <= len; ++dy)
+        res += ((C.c2d * (col[(int64_t)dy * p] - ui)) * C.dh2);
+    }
   }
   if (SUMONLY) {
     R.un[(int64_t)y * p + x] = res;
@@ -74,21 +86,82 @@ __global__ __launch_bounds__(256) void k_exact(RectList L, StepConst C) {
     const double sxv = C.sxt[gx + E], syv = C.syt[gy + E];
     double r2 = -((C.st2pi * sxv) * syv);
     const double wpos = (C.ct * sxv) * syv;
+    int n = 0;
     for (int dx = -E; dx <= E; ++dx) {
       const int len = C.lens[dx < 0 ? -dx : dx];
       const int sx = gx + dx;
       const bool inx = (sx >= 0) && (sx < C.nx);
       const double cx = C.ct * C.sxt[sx + E];
-      for (int dy = -len; dy <= len; ++dy) {
+      for (int dy = -len; dy <= len; ++dy, ++n) {
         const int sy = gy + dy;
         const bool in = inx && (sy >= 0) && (sy < C.ny);
         const double wv = in ? (cx * C.syt[sy + E]) : 0.0;
-        r2 -= ((C.c2d * (wv - wpos)) * C.dh2);
+        r2 -= (((WT ? C.wt[n] : C.c2d) * (wv - wpos)) * C.dh2);
       }
     }
     out += r2 * C.dt;
   }
   R.un[(int64_t)y * p + x] = out;
+}
+
+// ----------------------------------------------------------------------------
+// k_weighted: fast path for a non-constant radial J (influence != 0).  The
+// nested-window kernels need J = 1; here each 256-thread workgroup stages a
+// (64+2E) x (16+2E) tile of u in LDS (rows past the block clamp to its last
+// halo row; they only feed outputs that are not stored) and each thread
+// computes 4 outputs of one column:
+//   S = J00 u + sum_{groups} J(dx,dy) * (sum of the <= 4 mirror points)
+// (the disk |dy| <= len(|dx|) is symmetric in the signs of dx and dy), then
+// u' = u + alpha (S - Jsum u)  [+ dt b in test mode, b from L_h^J[W0]].
+template <bool TEST>
+__global__ __launch_bounds__(256) void k_weighted(RectList L, StepConst C) {
+  extern __shared__ double tile[];
+  const int work = xcd_remap(blockIdx.x, gridDim.x);
+  const int ri = find_rect(L, work);
+  const Rect &R = L.r[ri];
+  const int local = work - R.wg_begin;
+  const int tx = local % R.nstrip, ty = local / R.nstrip;
+  const int E = C.E;
+  const int x0 = R.x0 + tx * 64, y0 = R.y0 + ty * 16;
+  const int TW = 64 + 2 * E, TH = 16 + 2 * E;
+  const int64_t p = R.pitch;
+  // the block's allocation holds rows -E .. R.y1 + E - 1 of every rect in it
+  const int ylast = R.y1 + E - 1;
+  for (int e = (int)threadIdx.x; e < TW * TH; e += 256) {
+    const int r = e / TW, cc = e - r * TW;
+    const int gy = min(y0 - E + r, ylast);
+    tile[e] = R.u[(int64_t)gy * p + (x0 - E + cc)];
+  }
+  __syncthreads();
+  const int lx = (int)(threadIdx.x & 63), ly = (int)(threadIdx.x >> 6);
+  const int x = x0 + lx;
+  const double alpha = C.alpha, jsum = C.jsum;
+  const int EW = E + 1;
+  for (int k = 0; k < 4; ++k) {
+    const int oy = ly + 4 * k;
+    const int y = y0 + oy;
+    if (x >= R.x1 || y >= R.y1) continue;
+    const double *c = tile + (oy + E) * TW + (lx + E);
+    const double uc = c[0];
+    double s = C.qj[0] * uc;
+    for (int dx = 1; dx <= E; ++dx) s = fma(C.qj[dx * EW], c[dx] + c[-dx], s);
+    for (int dy = 1; dy <= E; ++dy) s = fma(C.qj[dy], c[dy * TW] + c[-dy * TW], s);
+    for (int dx = 1; dx <= E; ++dx) {
+      const int len = C.lens[dx];
+      for (int dy = 1; dy <= len; ++dy) {
+        const double *a = c + dy * TW, *b = c - dy * TW;
+        s = fma(C.qj[dx * EW + dy], (a[dx] + a[-dx]) + (b[dx] + b[-dx]), s);
+      }
+    }
+    double out = fma(alpha, fma(-jsum, uc, s), uc);
+    if (TEST) {
+      const int gx = R.gx0 + x, gyy = R.gy0 + y;
+      const double w0 = C.sxt[gx + E] * C.syt[gyy + E];
+      const double bsrc = -(C.st2pi * w0) - C.ct * R.lw[(int64_t)y * p + x];
+      out = fma(bsrc, C.dt, out);
+    }
+    R.un[(int64_t)y * p + x] = out;
+  }
 }
 
 // ----------------------------------------------------------------------------
@@ -335,16 +408,36 @@ int launch_fast(const RectList &rl, const StepConst &c, bool test, int want_r, v
 
 int launch_exact(const RectList &rl, const StepConst &c, bool test, void *stream) {
   hipStream_t st = (hipStream_t)stream;
-  if (test)
-    hipLaunchKernelGGL((k_exact<true, false>), dim3(rl.nwork), dim3(256), 0, st, rl, c);
+  const bool wt = c.influence != 0;
+  if (test && wt)
+    hipLaunchKernelGGL((k_exact<true, false, true>), dim3(rl.nwork), dim3(256), 0, st, rl, c);
+  else if (test)
+    hipLaunchKernelGGL((k_exact<true, false, false>), dim3(rl.nwork), dim3(256), 0, st, rl, c);
+  else if (wt)
+    hipLaunchKernelGGL((k_exact<false, false, true>), dim3(rl.nwork), dim3(256), 0, st, rl, c);
   else
-    hipLaunchKernelGGL((k_exact<false, false>), dim3(rl.nwork), dim3(256), 0, st, rl, c);
+    hipLaunchKernelGGL((k_exact<false, false, false>), dim3(rl.nwork), dim3(256), 0, st, rl, c);
   return check_launch();
 }
 
 int launch_exact_sum(const RectList &rl, const StepConst &c, void *stream) {
-  hipLaunchKernelGGL((k_exact<false, true>), dim3(rl.nwork), dim3(256), 0,
-                     (hipStream_t)stream, rl, c);
+  if (c.influence != 0)
+    hipLaunchKernelGGL((k_exact<false, true, true>), dim3(rl.nwork), dim3(256), 0,
+                       (hipStream_t)stream, rl, c);
+  else
+    hipLaunchKernelGGL((k_exact<false, true, false>), dim3(rl.nwork), dim3(256), 0,
+                       (hipStream_t)stream, rl, c);
+  return check_launch();
+}
+
+bool weighted_supported(int E) { return E >= 1 && E <= 32; }
+
+int launch_weighted(const RectList &rl, const StepConst &c, bool test, void *stream) {
+  const size_t shm = (size_t)(64 + 2 * c.E) * (16 + 2 * c.E) * sizeof(double);
+  if (test)
+    hipLaunchKernelGGL((k_weighted<true>), dim3(rl.nwork), dim3(256), shm, (hipStream_t)stream, rl, c);
+  else
+    hipLaunchKernelGGL((k_weighted<false>), dim3(rl.nwork), dim3(256), shm, (hipStream_t)stream, rl, c);
   return check_launch();
 }
 

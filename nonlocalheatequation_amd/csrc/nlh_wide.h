@@ -36,7 +36,7 @@
 
 namespace nlh {
 
-constexpr int kWideC = 8;    // rows per chunk (unroll; 8 measured fastest at E = 32)
+constexpr int kWideC = 12;   // rows per chunk (unroll; profiles/r02/wide_bench_7.jsonl)
 constexpr int kWideD = 6;    // input rows in flight
 constexpr int kWideLG = 4;   // window levels per LDS read group
 
@@ -71,16 +71,17 @@ __device__ __forceinline__ double tree_sum(const double (&p)[N]) {
 }
 
 // ABL (diagnostics, timing only): 1 = a scheduling barrier between rows
-template <int E, int CH, bool TEST, int D = kWideD, int ABL = 0, int PIN = 1, bool AB = false>
+template <int E, int CH, bool TEST, int D = kWideD, int ABL = 0, int PIN = 1, bool AB = false, int OBP = 16,
+          bool SPLIT8 = true>
 __global__ __launch_bounds__(64, 1) void k_wide(RectList L, StepConst C) {
   constexpr int W = 64;                 // output columns per strip
   constexpr int EP = (E + 1) & ~1;      // staged halo columns per side (16-B rows)
   constexpr int RW = W + 2 * EP;        // staged doubles per ring row
   constexpr int NCH = RW / 2;           // 16-byte chunks per row
-  // AB: every row staged twice, copy B one column later than copy A and 16
-  // bytes further in LDS (so a lane pair reading A and B hits different banks)
-  constexpr int RWS = AB ? 2 * RW + 4 : RW;  // doubles per ring slot
-  constexpr int OB = RW + 2;                 // copy B within a slot
+  // AB: every row staged twice, copy B one column later than copy A and
+  // OBP doubles further in LDS, shifting the banks the odd lanes read
+  constexpr int RWS = AB ? 2 * RW + 2 * OBP : RW;  // doubles per ring slot
+  constexpr int OB = RW + OBP;                     // copy B within a slot
   constexpr int K = pow2_ceil(D + 1);   // ring slots
   constexpr int GU = (AB ? 2 : 1) * ((NCH + 63) / 64);  // DMA instructions per u row
   constexpr int GL = TEST ? (W / 2 + 63) / 64 : 0;  // per L_h[W0] row
@@ -206,6 +207,21 @@ __global__ __launch_bounds__(64, 1) void k_wide(RectList L, StepConst C) {
             if (L0 + t <= E) {
               wl[g][t] = lv[E - (L0 + t) - 2 * lk0];
               wr[g][t] = rv[E + (L0 + t) - 2 * rk0];
+            }
+          }
+        } else if constexpr (SPLIT8) {
+          // separate ds_read_b64 (2 LDS cycles per wave-instruction): a memory
+          // barrier between the reads keeps the compiler from pairing them into
+          // ds_read2_b64 (8 cycles for the same bytes); the kernel is LDS-bound
+          // (SQ_LDS_IDX_ACTIVE 86% of cycles with the pairs, 548 vs 612 us per
+          // step at 8192^2, eps 32 without them)
+#pragma unroll
+          for (int t = 0; t < kWideLG; ++t) {
+            if (L0 + t <= E) {
+              wl[g][t] = wrow[E - (L0 + t)];
+              asm volatile("" ::: "memory");
+              wr[g][t] = wrow[E + (L0 + t)];
+              asm volatile("" ::: "memory");
             }
           }
         } else {

@@ -4,7 +4,7 @@
  * Plain-C restatement of the reference serial solver
  *   /root/reference/src/2d_nonlocal_serial.cpp
  * with the per-term floating-point operation order kept exactly:
- *   sum_local       :256-270   res += ((1.0*c_2d)*(u_j - u_i))*(dh*dh)
+ *   sum_local       :256-270   res += ((J*c_2d)*(u_j - u_i))*(dh*dh), J = influence_function = 1.0
  *   sum_local_test  :235-252   res  = -(((2pi*sin(2pi*(t*dt)))*sin(2pi*(x*dh)))*sin(2pi*(y*dh)))
  *                              res -= ((1.0*c_2d)*(w~_j - w_i))*(dh*dh)
  *   w               :207-210   (cos(2pi*(t*dt))*sin(2pi*(x*dh)))*sin(2pi*(y*dh))
@@ -32,7 +32,13 @@
 #endif
 
 double nlh_oracle_c2d(const nlh_oracle_params *p) {
+  if (p->influence == 1) return (p->k * 40) / pow(p->eps * p->dh, 4);
   return (p->k * 8) / pow(p->eps * p->dh, 4);
+}
+
+double nlh_oracle_influence(const nlh_oracle_params *p, long dx, long dy) {
+  if (p->influence == 1) return 1.0 - sqrt((double)(dx * dx + dy * dy)) / (double)p->eps;
+  return 1.0;
 }
 
 static long line_len(long eps, long dx) {
@@ -83,7 +89,7 @@ static double sum_local(const step_ctx *c, const double *u, long x, long y) {
     const int inx = (sx >= 0 && sx < nx);
     for (long sy = y - len; sy <= y + len; ++sy) {
       const double v = (inx && sy >= 0 && sy < ny) ? u[sx + sy * nx] : 0.0;
-      res += ((1.0 * c->c2d) * (v - ui)) * c->dh2;
+      res += ((nlh_oracle_influence(c->p, sx - x, sy - y) * c->c2d) * (v - ui)) * c->dh2;
     }
   }
   return res;
@@ -101,7 +107,7 @@ static double sum_local_test(const step_ctx *c, long x, long y) {
     for (long sy = y - len; sy <= y + len; ++sy) {
       const double wv =
           (inx && sy >= 0 && sy < ny) ? c->ct * c->sx_tab[sx + eps] * c->sy_tab[sy + eps] : 0.0;
-      res -= ((1.0 * c->c2d) * (wv - wpos)) * c->dh2;
+      res -= ((nlh_oracle_influence(c->p, sx - x, sy - y) * c->c2d) * (wv - wpos)) * c->dh2;
     }
   }
   return res;

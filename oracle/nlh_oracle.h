@@ -27,10 +27,22 @@ typedef struct {
   double dt;     /* time step                                              */
   double dh;     /* lattice spacing                                        */
   int test;      /* 1: add manufactured source (sum_local_test)            */
+  int influence; /* J(r), r = |y-x|/eps: 0 = 1 (the reference's            */
+                 /* influence_function, :201), 1 = 1 - r                   */
 } nlh_oracle_params;
 
-/* c_2d = (k*8)/pow(eps*dh,4)   -- src/2d_nonlocal_serial.cpp:76 */
+/* c_2d = (k*8)/pow(eps*dh,4)   -- src/2d_nonlocal_serial.cpp:76, which is
+ * 2k/(M3 (eps dh)^4) for J = 1 (M3 = 1/4; the spec's pi omitted as in the
+ * code).  General J (description/problem_description.tex:149-159): the same
+ * expression with 2/M3 in place of 8 -- J = 1 - r: M3 = 1/20, (k*40).       */
 double nlh_oracle_c2d(const nlh_oracle_params *p);
+
+/* J(distance/eps) for a neighbour at lattice offset (dx, dy), with the
+ * reference's distance() = sqrt(dx^2 + dy^2) (:224-227).  J = 1 returns 1.0,
+ * so the reference's per-term product ((J*c)*(u_j-u_i))*(dh*dh) is unchanged.
+ * PARITY UNPINNED for influence != 0: the reference only ever evaluates J = 1
+ * (no fixture exists for another J); this restatement follows the spec.     */
+double nlh_oracle_influence(const nlh_oracle_params *p, long dx, long dy);
 
 /* number of lattice points in the closed disk dx^2+dy^2 <= eps^2, counted the
  * way the reference loops (len_1d_line truncation, :231,260-262)            */

@@ -27,6 +27,7 @@ class Params(ctypes.Structure):
         ("dt", ctypes.c_double),
         ("dh", ctypes.c_double),
         ("test", ctypes.c_int),
+        ("influence", ctypes.c_int),
     ]
 
 
@@ -65,8 +66,9 @@ def _dp(a: np.ndarray):
     return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
 
 
-def params(nx, ny, eps, k, dt, dh, test) -> Params:
-    return Params(int(nx), int(ny), int(eps), float(k), float(dt), float(dh), int(bool(test)))
+def params(nx, ny, eps, k, dt, dh, test, influence=0) -> Params:
+    """influence: 0 = J = 1 (the reference), 1 = J(r) = 1 - r (parity unpinned)."""
+    return Params(int(nx), int(ny), int(eps), float(k), float(dt), float(dh), int(bool(test)), int(influence))
 
 
 def default_threads() -> int:

@@ -143,3 +143,15 @@ def test_distributed_small_tile_warning():
 def test_hpx_flags_ignored():
     out = run("2d_nonlocal_serial", ["--hpx:threads=4", "--test", "--cmp", "false", "--nt", "2"])
     assert "l2:" in out
+
+
+def test_serial_linear_influence_flag(oracle):
+    """--influence linear (extra flag): J(r) = 1 - r with c from M3 = 1/20."""
+    out = run("2d_nonlocal_serial", ["--test", "--cmp", "false", "--nt", "10", "--nlog", "1000",
+                                     "--influence", "linear", "--kernel", "exact"])
+    p = oracle.params(50, 50, 5, 1.0, 0.0005, 0.02, 1, 1)
+    l2, li = oracle.errors(p, 10, oracle.run(p, 10))
+    assert out.splitlines()[1] == f"l2: {l2:g} linfinity: {li:g}"
+    p = subprocess.run([os.path.join(BIN, "2d_nonlocal_serial"), "--influence", "quadratic"],
+                       capture_output=True, text=True, timeout=60)
+    assert p.returncode != 0

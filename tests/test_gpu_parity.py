@@ -284,3 +284,88 @@ def test_pair_split_bitwise_equals_one_wave_pair(monkeypatch, eps):
 def test_pair_not_used_where_single_step_is_faster(eps):
     with N.Solver(300, 200, eps, 1.0, 1e-9, 1.0 / 300, test=False, kernel="fast") as s:
         assert s.info().steps_per_pass == 1 and s.info().halo_width == eps
+
+
+def _oracle_run_j(O, r, test, influence, u0=None):
+    p = O.params(r.nx, r.ny, r.eps, r.k, r.dt, r.dh, test, influence)
+    u = O.run(p, r.nt, u0)
+    l2, li = O.errors(p, r.nt, u)
+    return u, l2, li
+
+
+def _gpu_run_j(r, test, kernel, influence, u0=None, **kw):
+    with N.Solver(r.nx, r.ny, r.eps, r.k, r.dt, r.dh, test=test, kernel=kernel, influence=influence,
+                  **kw) as s:
+        if u0 is None:
+            s.test_init()
+        else:
+            s.input_init(u0)
+        s.run(r.nt)
+        s.synchronize()
+        return s.field(), s.errors(r.nt), s.info()
+
+
+@pytest.mark.parametrize("eps", [3, 5, 8, 17])
+@pytest.mark.parametrize("test", [False, True])
+def test_linear_influence_exact_bitwise(oracle, eps, test):
+    """J(r) = 1 - r (problem_description.tex:159; c from M3 = 1/20): the exact
+    kernel's per-point J*c table keeps the reference's per-term order,
+    bitwise equal to the oracle extension (parity unpinned: the reference only
+    evaluates J = 1)."""
+    nx, ny, nt = 90, 70, 5
+    dh = 1.0 / nx
+    r = N.BatchRow(nx, ny, nt, eps, 0.5, 0.3 * eps ** 4 * dh * dh / N.disk_count(eps), dh)
+    u0 = None if test else np.random.default_rng(eps).uniform(-1, 1, size=(ny, nx))
+    u_ref, l2_ref, li_ref = _oracle_run_j(oracle, r, test, 1, u0)
+    u, (l2, li), info = _gpu_run_j(r, test, "exact", "linear", u0)
+    assert info.kernel == N.KERNEL_EXACT
+    assert np.array_equal(u.view(np.uint64), u_ref.view(np.uint64))
+    if test:
+        assert li == li_ref and abs(l2 - l2_ref) <= 1e-13 * l2_ref
+
+
+@pytest.mark.parametrize("eps", [3, 8, 17, 32])
+@pytest.mark.parametrize("test", [False, True])
+def test_linear_influence_weighted_fast(oracle, eps, test):
+    """k_weighted (AUTO for J != 1): the symmetric-group FMA sum over an LDS
+    tile, within 1e-12 of field scale per node and 1e-10 in L2; ragged
+    lattice so strips and 16-row segments are partial."""
+    nx, ny, nt = 150, 133, 4
+    dh = 1.0 / nx
+    r = N.BatchRow(nx, ny, nt, eps, 1.0, 0.5 * eps ** 4 * dh * dh / N.disk_count(eps), dh)
+    u0 = None if test else np.random.default_rng(70 + eps).uniform(-1, 1, size=(ny, nx))
+    u_ref, l2_ref, _ = _oracle_run_j(oracle, r, test, 1, u0)
+    u, (l2, _), info = _gpu_run_j(r, test, "auto", "linear", u0)
+    assert info.pass_kernel == "k_weighted" and info.kernel == N.KERNEL_FAST
+    d = np.max(np.abs(u - u_ref))
+    assert d <= 1e-12 * np.max(np.abs(u_ref))
+    if test:
+        # with the consistent source, u - w is near the rounding floor here
+        # (l2 ~ 1e-10 .. 1e-6), so on top of 1e-10 relative allow the L2 change
+        # the per-node difference d implies: |sum a^2 - sum b^2| <= d (2 sqrt(n l2) + n d)
+        n = nx * ny
+        assert abs(l2 - l2_ref) <= 1e-10 * l2_ref + d * (2 * np.sqrt(n * l2_ref) + n * d)
+
+
+def test_linear_influence_multiblock_rccl_self(oracle, monkeypatch):
+    """J = 1 - r through the multi-block exchange (NLH_RCCL_SELF, 3 x 2 tiles):
+    exact bitwise, weighted fast within tolerance."""
+    monkeypatch.setenv("NLH_RCCL_SELF", "1")
+    nx, ny, eps, nt = 192, 128, 6, 4
+    dh = 1.0 / nx
+    r = N.BatchRow(nx, ny, nt, eps, 1.0, 0.5 * eps ** 4 * dh * dh / N.disk_count(eps), dh)
+    u0 = np.random.default_rng(9).uniform(-1, 1, size=(ny, nx))
+    u_ref, _, _ = _oracle_run_j(oracle, r, False, 1, u0)
+    ue, _, info = _gpu_run_j(r, False, "exact", "linear", u0, tiles=(3, 2), split_tiles=True)
+    assert info.nblocks == 6 and info.npeers == 1
+    assert np.array_equal(ue, u_ref)
+    uf, _, info = _gpu_run_j(r, False, "fast", "linear", u0, tiles=(3, 2), split_tiles=True)
+    assert info.pass_kernel == "k_weighted"
+    assert np.max(np.abs(uf - u_ref)) <= 1e-12 * np.max(np.abs(u_ref))
+
+
+def test_linear_influence_large_eps_uses_exact():
+    with N.Solver(100, 90, 40, 1.0, 1e-9, 0.01, influence="linear") as s:
+        assert s.info().kernel == N.KERNEL_EXACT
+    with pytest.raises(N.NLHError):
+        N.Solver(100, 90, 40, 1.0, 1e-9, 0.01, influence="linear", kernel="fast")

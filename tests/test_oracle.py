@@ -126,3 +126,25 @@ def test_stdin_ic_order(oracle):
             u[sx + sy * nx] = stream[i]
             i += 1
     assert list(u) == [0, 2, 4, 1, 3, 5]
+
+
+def test_linear_influence_restatement(oracle):
+    """J(r) = 1 - r extension (problem_description.tex:149-159): c from M3 =
+    1/20 (2/M3 = 40 in place of the reference's 8, pi omitted as :76), J = 1
+    at the centre, 0 on the horizon; the J = 1 path is the pinned reference."""
+    p1 = oracle.params(40, 30, 5, 1.0, 1e-4, 0.02, 0, 1)
+    p0 = oracle.params(40, 30, 5, 1.0, 1e-4, 0.02, 0, 0)
+    assert oracle.c2d(p1) == (1.0 * 40) / (5 * 0.02) ** 4
+    assert oracle.c2d(p0) == (1.0 * 8) / (5 * 0.02) ** 4
+    L = oracle.lib()
+    import ctypes
+    L.nlh_oracle_influence.argtypes = [ctypes.POINTER(type(p1)), ctypes.c_long, ctypes.c_long]
+    L.nlh_oracle_influence.restype = ctypes.c_double
+    assert L.nlh_oracle_influence(ctypes.byref(p1), 0, 0) == 1.0
+    assert L.nlh_oracle_influence(ctypes.byref(p1), 3, 4) == 0.0
+    assert L.nlh_oracle_influence(ctypes.byref(p0), 3, 4) == 1.0
+    # a constant field is a fixed point of the operator away from the
+    # boundary for any J (sum of J (u_j - u_i) = 0)
+    u = np.ones((30, 40))
+    un = oracle.step(p1, 0, u)
+    assert np.allclose(un[10:20, 10:30], 1.0, rtol=0, atol=1e-15)

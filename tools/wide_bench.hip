@@ -74,11 +74,9 @@ int main(int argc, char **argv) {
   CK(hipGetDeviceProperties(&prop, 0));
   const int cus = prop.multiProcessorCount;
   std::vector<Variant> vs = {
-      {"fast_R1_D6", k_fast<E, 1, 6, false>, 64, 4},
       {"wide_C8_D6", k_wide<E, 8, false, 6, 0, 1>, 64, 8},
-      {"wide_C8_D6_AB", k_wide<E, 8, false, 6, 0, 1, true>, 64, 8},
-      {"wide_C12_D6_AB", k_wide<E, 12, false, 6, 0, 1, true>, 64, 8},
-      {"wide_C8_D4_AB", k_wide<E, 8, false, 4, 0, 1, true>, 64, 8},
+      {"wide_C8_D6_split8", k_wide<E, 8, false, 6, 0, 1, false, 16, true>, 64, 8},
+      {"wide_C12_D6_split8", k_wide<E, 12, false, 6, 0, 1, false, 16, true>, 64, 8},
   };
   std::vector<double> ref((size_t)n * n), got((size_t)n * n);
   hipEvent_t e0, e1;
