@@ -1,6 +1,6 @@
 # Build of the MI355X-native nonlocal heat-equation solver.
 #   libnlh.so   C-ABI solver library (HIP kernels for gfx950 + RCCL)
-#   bin/2d_nonlocal_{serial,async,distributed}   drop-in CLI drivers
+#   bin/2d_nonlocal_{serial,async,distributed}, bin/1d_nonlocal_serial   drop-in CLI drivers
 #   oracle/liboracle.so   CPU checker (test infrastructure only)
 ROCM    ?= /opt/rocm
 HIPCC   ?= $(ROCM)/bin/hipcc
@@ -19,11 +19,12 @@ HOSTFLAGS := -O2 $(CXXSTD) -fPIC $(WARN) $(INC) -D__HIP_PLATFORM_AMD__ -I$(ROCM)
 
 FAST_UNITS := $(sort $(wildcard $(CSRC)/nlh_fast_e*.hip $(CSRC)/nlh_pair_e*.hip $(CSRC)/nlh_wide_e*.hip))
 FAST_OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(FAST_UNITS))
-LIB_OBJS := $(OBJDIR)/nlh_kernels.o $(FAST_OBJS) $(OBJDIR)/nlh_api.o $(OBJDIR)/nlh_plan.o
+LIB_OBJS := $(OBJDIR)/nlh_kernels.o $(FAST_OBJS) $(OBJDIR)/nlh_api.o $(OBJDIR)/nlh_plan.o $(OBJDIR)/nlh_1d.o
 # the fast kernel is fully unrolled over 2E+1 rows; lift LLVM's pragma-unroll
 # size cap so every accumulator stays in registers (no scratch)
 UNROLL  := -mllvm -pragma-unroll-threshold=1000000
-DRIVERS  := $(BINDIR)/2d_nonlocal_serial $(BINDIR)/2d_nonlocal_async $(BINDIR)/2d_nonlocal_distributed
+DRIVERS  := $(BINDIR)/2d_nonlocal_serial $(BINDIR)/2d_nonlocal_async $(BINDIR)/2d_nonlocal_distributed \
+            $(BINDIR)/1d_nonlocal_serial
 DRV_COMMON := $(OBJDIR)/driver_common.o $(OBJDIR)/vtu_writer.o
 
 all: lib drivers oracle
@@ -51,6 +52,9 @@ $(OBJDIR)/nlh_wide_%.o: $(CSRC)/nlh_wide_%.hip $(CHDRS) $(CSRC)/nlh_wide.h | $(O
 	$(HIPCC) $(HIPFLAGS) $(UNROLL) -c $< -o $@
 
 $(OBJDIR)/nlh_api.o: $(CSRC)/nlh_api.cpp $(CSRC)/nlh_device.h $(CSRC)/nlh_plan.h include/nlh.h | $(OBJDIR)
+	$(HIPCC) $(HOSTFLAGS) -x c++ -c $< -o $@
+
+$(OBJDIR)/nlh_1d.o: $(CSRC)/nlh_1d.cpp include/nlh.h | $(OBJDIR)
 	$(HIPCC) $(HOSTFLAGS) -x c++ -c $< -o $@
 
 $(OBJDIR)/nlh_plan.o: $(CSRC)/nlh_plan.cpp $(CSRC)/nlh_plan.h | $(OBJDIR)

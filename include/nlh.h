@@ -188,6 +188,35 @@ int64_t nlh_halo_plan(const nlh_params *p, int64_t *pieces, int64_t cap);
  *   {rank, local_index, gx0, gy0, w, h}                                    */
 int64_t nlh_block_plan(const nlh_params *p, int64_t *blocks, int64_t cap);
 
+/* ---- 1D solver: drop-in for src/1d_nonlocal_serial.cpp --------------------
+ *   nlh1d_create      solver::solver(nx, nt, eps, nlog)   1d :54-87
+ *                     (c_1d = (long)((k*3)/pow(eps*dx,3)), `long` in the
+ *                      reference, :49,57 -- truncation kept)
+ *   nlh1d_init_test   test_init()                         1d :127-132
+ *   nlh1d_set_field   input_init()                        1d :119-125
+ *   nlh1d_run         do_work() time loop                 1d :237-262
+ *                     (sum_local :226-234, sum_local_test :214-223)
+ *   nlh1d_errors      compute_l2 / compute_linf           1d :91-103
+ * One thread per node, the reference's per-term order (bitwise); the 1D
+ * problem is small (the reference's batch rows have <= 1000 nodes).       */
+typedef struct nlh1d_params {
+  int64_t nx;         /* nodes                                              */
+  int64_t eps;        /* horizon in nodes (>= 1)                            */
+  double k, dt, dx;   /* heat coefficient, time step, spacing               */
+  int32_t test;       /* 1: manufactured-solution source                    */
+  int32_t device;     /* HIP device ordinal, -1 = current                   */
+} nlh1d_params;
+
+typedef struct nlh1d_solver nlh1d_solver;
+
+int nlh1d_create(const nlh1d_params *p, nlh1d_solver **out);
+int nlh1d_destroy(nlh1d_solver *s);
+int nlh1d_init_test(nlh1d_solver *s);                 /* u = sin(2 pi x dx); t := 0 */
+int nlh1d_set_field(nlh1d_solver *s, const double *u); /* nx doubles; t := 0        */
+int nlh1d_get_field(nlh1d_solver *s, double *u);
+int nlh1d_run(nlh1d_solver *s, int64_t nsteps);       /* synchronous                */
+int nlh1d_errors(nlh1d_solver *s, int64_t time, double *l2, double *linf);
+
 const char *nlh_last_error(void);
 int nlh_abi_version(void);
 

@@ -16,6 +16,8 @@ Reference correspondences::
     Solver.compute_l2(t)     solver::compute_l2(time)                   :96-103
     Solver.compute_linf(t)   solver::compute_linf(time)                 :106-113
     batch_tester(text)       batch_tester()                             :306-333
+    Solver1D(...)            src/1d_nonlocal_serial.cpp solver          :32-237
+    batch_tester_1d(text)    src/1d_nonlocal_serial.cpp batch_tester    :239-266
 """
 from __future__ import annotations
 
@@ -28,7 +30,7 @@ import numpy as np
 __all__ = [
     "KERNEL_AUTO", "KERNEL_EXACT", "KERNEL_FAST", "INFLUENCE_CONSTANT", "INFLUENCE_LINEAR", "NLHError", "Solver",
     "lib", "lib_path", "comm_unique_id", "resolve_owner", "halo_plan", "block_plan",
-    "disk_count", "batch_tester", "BatchRow",
+    "disk_count", "batch_tester", "BatchRow", "Solver1D", "batch_tester_1d",
 ]
 
 KERNEL_AUTO, KERNEL_EXACT, KERNEL_FAST = 0, 1, 2
@@ -71,6 +73,14 @@ class _Info(ctypes.Structure):
     ]
 
 
+class _Params1D(ctypes.Structure):
+    _fields_ = [
+        ("nx", ctypes.c_int64), ("eps", ctypes.c_int64),
+        ("k", ctypes.c_double), ("dt", ctypes.c_double), ("dx", ctypes.c_double),
+        ("test", ctypes.c_int32), ("device", ctypes.c_int32),
+    ]
+
+
 # every symbol include/nlh.h declares, with its ctypes signature
 _SIGNATURES = {
     "nlh_abi_version": ([], ctypes.c_int),
@@ -100,6 +110,14 @@ _SIGNATURES = {
                       ctypes.c_int64),
     "nlh_block_plan": ([ctypes.POINTER(_Params), ctypes.POINTER(ctypes.c_int64), ctypes.c_int64],
                        ctypes.c_int64),
+    "nlh1d_create": ([ctypes.POINTER(_Params1D), ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
+    "nlh1d_destroy": ([ctypes.c_void_p], ctypes.c_int),
+    "nlh1d_init_test": ([ctypes.c_void_p], ctypes.c_int),
+    "nlh1d_set_field": ([ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
+    "nlh1d_get_field": ([ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
+    "nlh1d_run": ([ctypes.c_void_p, ctypes.c_int64], ctypes.c_int),
+    "nlh1d_errors": ([ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_double),
+                      ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
 }
 
 _lib = None
@@ -420,5 +438,94 @@ def batch_tester(text: str, fmt: str = "serial", kernel="auto") -> str:
             s.test_init()
             s.do_work(r.nt)
             if s.error_l2 / float(r.nx * r.ny) > 1e-6:
+                return "Tests Failed"
+    return "Tests Passed"
+
+
+class Solver1D:
+    """The 1D solver (src/1d_nonlocal_serial.cpp:32-237) on a GPU: nx nodes,
+    horizon eps nodes, c = (long)(3k / (eps dx)^3) as the reference truncates
+    it (:57,74), zero nodes outside [0, nx) (boundary(), :178-183)."""
+
+    def __init__(self, nx, eps, k=1.0, dt=0.001, dx=0.02, *, test=False, device=-1):
+        self.nx, self.eps = int(nx), int(eps)
+        self.k, self.dt, self.dx = float(k), float(dt), float(dx)
+        self.test = bool(test)
+        self.error_l2 = 0.0
+        self.error_linf = 0.0
+        self.t = 0
+        p = _Params1D(self.nx, self.eps, self.k, self.dt, self.dx, int(self.test), int(device))
+        h = ctypes.c_void_p()
+        _check(lib().nlh1d_create(ctypes.byref(p), ctypes.byref(h)), "nlh1d_create")
+        self._h = h
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            lib().nlh1d_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def test_init(self) -> None:
+        """u(x, 0) = sin(2 pi x dx) (test_init, :124-129); the source term is
+        fixed at construction (``test=``)."""
+        _check(lib().nlh1d_init_test(self._h), "nlh1d_init_test")
+        self.t = 0
+
+    def input_init(self, u: np.ndarray) -> None:
+        u = np.ascontiguousarray(u, dtype=np.float64).reshape(self.nx)
+        _check(lib().nlh1d_set_field(self._h, _dp(u)), "nlh1d_set_field")
+        self.t = 0
+
+    def run(self, nsteps: int) -> None:
+        _check(lib().nlh1d_run(self._h, int(nsteps)), "nlh1d_run")
+        self.t += int(nsteps)
+
+    def do_work(self, nt: int) -> None:
+        """Advance nt steps; in test mode set error_l2/error_linf at the
+        final time (do_work :209-236)."""
+        self.run(nt)
+        if self.test:
+            self.error_l2, self.error_linf = self.errors(self.t)
+
+    def errors(self, time: int):
+        l2 = ctypes.c_double()
+        li = ctypes.c_double()
+        _check(lib().nlh1d_errors(self._h, int(time), ctypes.byref(l2), ctypes.byref(li)), "nlh1d_errors")
+        return l2.value, li.value
+
+    def field(self) -> np.ndarray:
+        out = np.zeros(self.nx, dtype=np.float64)
+        _check(lib().nlh1d_get_field(self._h, _dp(out)), "nlh1d_get_field")
+        return out
+
+
+def parse_batch_1d(text: str):
+    """tests/1d.txt: num_tests, then rows "nx nt eps k dt dx" (1d :239-245)."""
+    tok = text.split()
+    rows = []
+    for i in range(int(tok[0])):
+        f = tok[1 + 6 * i: 7 + 6 * i]
+        rows.append((int(f[0]), int(f[1]), int(f[2]), float(f[3]), float(f[4]), float(f[5])))
+    return rows
+
+
+def batch_tester_1d(text: str) -> str:
+    """"Tests Passed" iff every row has error_l2 / nx <= 1e-6 (1d :239-264)."""
+    for nx, nt, eps, k, dt, dx in parse_batch_1d(text):
+        with Solver1D(nx, eps, k, dt, dx, test=True) as s:
+            s.test_init()
+            s.do_work(nt)
+            if s.error_l2 / float(nx) > 1e-6:
                 return "Tests Failed"
     return "Tests Passed"

@@ -120,6 +120,17 @@ void print_time_results(uint32_t localities, uint64_t threads, uint64_t elapsed_
   std::fflush(stdout);
 }
 
+void print_time_results(uint64_t threads, uint64_t elapsed_ns, uint64_t nx, uint64_t nt, bool header) {
+  if (header)
+    std::cout << "OS_Threads,       Execution_Time_sec,"
+                 "       x dimension,        y dimension,        Time_Steps\n"
+              << std::flush;
+  const std::string t = std::to_string(threads) + ",", x = std::to_string(nx) + ",",
+                    n = std::to_string(nt) + " ";
+  std::printf("%-21s %10.12lf,        %-21s %-21s\n", t.c_str(), elapsed_ns / 1e9, x.c_str(), n.c_str());
+  std::fflush(stdout);
+}
+
 void print_errors(double l2, double linf) {
   std::cout << "l2: " << l2 << " linfinity: " << linf << std::endl;
 }

@@ -49,6 +49,9 @@ void print_time_results(uint32_t localities, uint64_t threads, uint64_t elapsed_
                         uint64_t nx, uint64_t ny, uint64_t npx, uint64_t npy, uint64_t nt,
                         bool header);
 
+// include/print_time_results.hpp:84-99 (1d)
+void print_time_results(uint64_t threads, uint64_t elapsed_ns, uint64_t nx, uint64_t nt, bool header);
+
 uint64_t now_ns();
 
 struct RankEnv {

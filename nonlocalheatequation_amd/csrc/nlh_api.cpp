@@ -40,6 +40,18 @@ int fail(int code, const std::string &msg) {
   return code;
 }
 
+}  // namespace
+
+namespace nlh {
+// the 1D solver's entry points (nlh_1d.cpp) report through nlh_last_error too
+const char *set_last_error(const std::string &msg) {
+  g_err = msg;
+  return g_err.c_str();
+}
+}  // namespace nlh
+
+namespace {
+
 #define HIP_TRY(expr)                                                        \
   do {                                                                       \
     hipError_t e_ = (expr);                                                  \

@@ -165,6 +165,69 @@ __global__ __launch_bounds__(256) void k_weighted(RectList L, StepConst C) {
 }
 
 // ----------------------------------------------------------------------------
+// 1D solver (src/1d_nonlocal_serial.cpp): one thread per node, the
+// reference's per-term order; u has eps zero nodes on each side
+template <bool TEST>
+__global__ __launch_bounds__(256) void k_1d(const double *u, double *un, int64_t nx, int eps, double c,
+                                            double dt, double dx, double st2pi, double ct,
+                                            const double *sxt) {
+#pragma clang fp contract(off)
+  const int64_t x = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (x >= nx) return;
+  const double ui = u[x];
+  double res = 0.0;  // sum_local (1d :226-234)
+  for (int d = -eps; d <= eps; ++d) res += ((1.0 * c) * (u[x + d] - ui)) * dx;
+  double out = ui + (res * dt);
+  if (TEST) {  // sum_local_test (1d :214-223), w from the host sin table
+    double r2 = -(st2pi * sxt[x + eps]);
+    const double wpos = ct * sxt[x + eps];
+    for (int d = -eps; d <= eps; ++d) {
+      const int64_t sx = x + d;
+      const double wv = (sx >= 0 && sx < nx) ? ct * sxt[sx + eps] : 0.0;
+      r2 -= ((1.0 * c) * (wv - wpos)) * dx;
+    }
+    out += r2 * dt;
+  }
+  un[x] = out;
+}
+
+// compute_l2 / compute_linf (1d :91-103) in the reference's sequential order
+// (one thread; the 1D lattices are small)
+__global__ void k_1d_norms(const double *u, int64_t nx, int eps, double ct, const double *sxt,
+                           double *out) {
+#pragma clang fp contract(off)
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  double e2 = 0.0, ei = 0.0;
+  for (int64_t x = 0; x < nx; ++x) {
+    const double d = u[x] - ct * sxt[x + eps];
+    e2 += d * d;
+    ei = fmax(fabs(d), ei);
+  }
+  out[0] = e2;
+  out[1] = ei;
+}
+
+int launch_1d(const double *u, double *un, int64_t nx, int32_t eps, double c1d, double dt, double dx,
+              bool test, double st2pi, double ct, const double *sxt, void *stream) {
+  const dim3 grid((unsigned)((nx + 255) / 256));
+  if (test)
+    hipLaunchKernelGGL(k_1d<true>, grid, dim3(256), 0, (hipStream_t)stream, u, un, nx, eps, c1d, dt, dx,
+                       st2pi, ct, sxt);
+  else
+    hipLaunchKernelGGL(k_1d<false>, grid, dim3(256), 0, (hipStream_t)stream, u, un, nx, eps, c1d, dt, dx,
+                       st2pi, ct, sxt);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : (int)e;
+}
+
+int launch_1d_norms(const double *u, int64_t nx, int32_t eps, double ct, const double *sxt, double *out,
+                    void *stream) {
+  hipLaunchKernelGGL(k_1d_norms, dim3(1), dim3(64), 0, (hipStream_t)stream, u, nx, eps, ct, sxt, out);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : (int)e;
+}
+
+// ----------------------------------------------------------------------------
 // halo copies
 __global__ __launch_bounds__(256) void k_copies(CopyList L) {
   const int work = blockIdx.x;

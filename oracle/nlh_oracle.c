@@ -267,3 +267,59 @@ double nlh_oracle_run_tiled(const nlh_oracle_params *p, long nt, long tiles_x,
   free(b);
   return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
 }
+
+/* ------------------------------------------------------------------------- */
+/* 1D solver (src/1d_nonlocal_serial.cpp)                                      */
+double nlh_oracle_c1d(long eps, double k, double dx) {
+  const long c = (long)((k * 3) / (pow(eps * dx, 3))); /* `long c_1d` (:49,57) */
+  return (double)c;
+}
+
+void nlh_oracle_run_1d(long nx, long nt, long eps, double k, double dt, double dx, int test,
+                       double *u) {
+  const double c = nlh_oracle_c1d(eps, k, dx);
+  double *s[2];
+  s[0] = u;
+  s[1] = (double *)malloc(sizeof(double) * (size_t)(nx > 0 ? nx : 1));
+  double *sxt = sin_table(-eps, nx + eps, dx);
+  for (long t = 0; t < nt; ++t) {
+    const double *cur = s[t % 2];
+    double *nxt = s[(t + 1) % 2];
+    const double st = sin(2 * M_PI * (t * dt)), ct = cos(2 * M_PI * (t * dt));
+    for (long x = 0; x < nx; ++x) {
+      double res = 0.0;
+      for (long sx = x - eps; sx <= x + eps; ++sx) {
+        const double v = (sx >= 0 && sx < nx) ? cur[sx] : 0.0;
+        res += ((1.0 * c) * (v - cur[x])) * dx;
+      }
+      nxt[x] = cur[x] + (res * dt);
+      if (test) {
+        double r2 = -(((2 * M_PI) * st) * sxt[x + eps]);
+        const double wpos = ct * sxt[x + eps];
+        for (long sx = x - eps; sx <= x + eps; ++sx) {
+          const double wv = (sx >= 0 && sx < nx) ? ct * sxt[sx + eps] : 0.0;
+          r2 -= ((1.0 * c) * (wv - wpos)) * dx;
+        }
+        nxt[x] += r2 * dt;
+      }
+    }
+  }
+  if (nt % 2) memcpy(u, s[1], sizeof(double) * (size_t)nx);
+  free(s[1]);
+  free(sxt);
+}
+
+void nlh_oracle_errors_1d(long nx, long time, double dt, double dx, const double *u,
+                          double *l2, double *linf) {
+  const double ct = cos(2 * M_PI * (time * dt));
+  double e2 = 0, ei = 0;
+  for (long sx = 0; sx < nx; ++sx) {
+    const double w = ct * sin(2 * M_PI * (sx * dx));
+    const double d = u[sx] - w;
+    e2 += d * d;
+    const double a = fabs(d);
+    ei = (a < ei) ? ei : a;
+  }
+  *l2 = e2;
+  *linf = ei;
+}

@@ -77,6 +77,19 @@ void nlh_oracle_errors(const nlh_oracle_params *p, long time, const double *u,
 double nlh_oracle_run_tiled(const nlh_oracle_params *p, long nt, long tiles_x,
                             long tiles_y, double *u, int nthreads);
 
+/* ---- 1D solver (src/1d_nonlocal_serial.cpp) --------------------------------
+ * c_1d is declared `long` in the reference (:49,57): (k*3)/pow(eps*dx,3) is
+ * truncated toward zero.  sum_local (:226-234): res += ((1.0*c_1d)*(u_j -
+ * u_i))*dx over sx = x-eps .. x+eps, 0 outside [0,nx); sum_local_test
+ * (:214-223): res = -(((2pi)*sin(2pi(t dt)))*sin(2pi(x dx))), res -=
+ * ((1.0*c_1d)*(w_j - w_i))*dx; do_work (:237-262): u' = u + res*dt, then
+ * u' += res_test*dt; compute_l2/linf (:91-103).                            */
+double nlh_oracle_c1d(long eps, double k, double dx);
+void nlh_oracle_run_1d(long nx, long nt, long eps, double k, double dt, double dx, int test,
+                       double *u);
+void nlh_oracle_errors_1d(long nx, long time, double dt, double dx, const double *u,
+                          double *l2, double *linf);
+
 #ifdef __cplusplus
 }
 #endif

@@ -9,6 +9,7 @@ citations) and is pinned against SURVEY.md Appendix A (tests/test_oracle.py).
 from __future__ import annotations
 
 import ctypes
+import math
 import os
 import subprocess
 
@@ -57,6 +58,12 @@ def lib() -> ctypes.CDLL:
         L.nlh_oracle_errors.argtypes = [P, ctypes.c_long, dp, dp, dp]
         L.nlh_oracle_run_tiled.argtypes = [P, ctypes.c_long, ctypes.c_long, ctypes.c_long, dp, ctypes.c_int]
         L.nlh_oracle_run_tiled.restype = ctypes.c_double
+        L.nlh_oracle_c1d.argtypes = [ctypes.c_long, ctypes.c_double, ctypes.c_double]
+        L.nlh_oracle_c1d.restype = ctypes.c_double
+        L.nlh_oracle_run_1d.argtypes = [ctypes.c_long, ctypes.c_long, ctypes.c_long, ctypes.c_double,
+                                        ctypes.c_double, ctypes.c_double, ctypes.c_int, dp]
+        L.nlh_oracle_errors_1d.argtypes = [ctypes.c_long, ctypes.c_long, ctypes.c_double, ctypes.c_double,
+                                           dp, dp, dp]
         _lib = L
     return _lib
 
@@ -121,3 +128,23 @@ def run_tiled(p: Params, nt: int, tiles_x: int, tiles_y: int, u: np.ndarray, nth
     """In-place tiled run (2d_nonlocal_async execution model); returns seconds."""
     assert u.dtype == np.float64 and u.flags.c_contiguous
     return lib().nlh_oracle_run_tiled(ctypes.byref(p), int(nt), int(tiles_x), int(tiles_y), _dp(u), int(nthreads))
+
+
+# ---- 1D solver (src/1d_nonlocal_serial.cpp) ---------------------------------
+def test_init_1d(nx: int, dx: float) -> np.ndarray:
+    """test_init(): sin(2*pi*(sx*dx)) (1d :127-132)."""
+    return np.array([math.sin(2 * math.pi * (sx * dx)) for sx in range(nx)], dtype=np.float64)  # libm sin
+
+
+def run_1d(nx, nt, eps, k, dt, dx, test, u=None) -> np.ndarray:
+    u = test_init_1d(nx, dx) if u is None else np.array(u, dtype=np.float64, copy=True)
+    lib().nlh_oracle_run_1d(int(nx), int(nt), int(eps), float(k), float(dt), float(dx), int(bool(test)), _dp(u))
+    return u
+
+
+def errors_1d(nx, time, dt, dx, u) -> tuple[float, float]:
+    u = np.ascontiguousarray(u, dtype=np.float64)
+    l2 = ctypes.c_double()
+    li = ctypes.c_double()
+    lib().nlh_oracle_errors_1d(int(nx), int(time), float(dt), float(dx), _dp(u), ctypes.byref(l2), ctypes.byref(li))
+    return l2.value, li.value

@@ -18,7 +18,7 @@ HEADER = os.path.join(ROOT, "include", "nlh.h")
 def declared_symbols():
     text = open(HEADER).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b(nlh_[a-z_]+)\s*\(", text)))
+    return sorted(set(re.findall(r"\b(nlh(?:1d)?_[a-z_]+)\s*\(", text)))
 
 
 def test_header_symbols_exported():
@@ -26,7 +26,7 @@ def test_header_symbols_exported():
     assert len(syms) >= 20
     out = subprocess.run(["nm", "-D", "--defined-only", N.lib_path()], capture_output=True,
                          text=True, check=True).stdout
-    exported = set(re.findall(r"\bT (nlh_\w+)", out))
+    exported = set(re.findall(r"\bT (nlh(?:1d)?_\w+)", out))
     missing = [s for s in syms if s not in exported]
     assert not missing, missing
 

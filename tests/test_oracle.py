@@ -148,3 +148,53 @@ def test_linear_influence_restatement(oracle):
     u = np.ones((30, 40))
     un = oracle.step(p1, 0, u)
     assert np.allclose(un[10:20, 10:30], 1.0, rtol=0, atol=1e-15)
+
+
+def test_oracle_1d_c_truncation(oracle):
+    # `long c_1d` (src/1d_nonlocal_serial.cpp:57,74) truncates 3k/(eps dx)^3:
+    # 2999.999... -> 2999 for the default flags, 0 for the last 1d.txt row
+    assert oracle.lib().nlh_oracle_c1d(5, 1.0, 0.02) == 2999.0
+    assert oracle.lib().nlh_oracle_c1d(40, 0.02, 0.016) == 0.0
+    assert oracle.lib().nlh_oracle_c1d(40, 0.5, 0.02) == 2.0
+
+
+def _parse_1d(text):
+    tok = text.split()
+    return [(int(tok[1 + 6 * i]), int(tok[2 + 6 * i]), int(tok[3 + 6 * i]), float(tok[4 + 6 * i]),
+             float(tok[5 + 6 * i]), float(tok[6 + 6 * i])) for i in range(int(tok[0]))]
+
+
+def test_oracle_1d_batch_contract(oracle):
+    """Test_1d (CMakeLists.txt:101): every tests/1d.txt row has l2/nx <= 1e-6."""
+    for nx, nt, eps, k, dt, dx in _parse_1d(read_input("1d.txt")):
+        u = oracle.run_1d(nx, nt, eps, k, dt, dx, True)
+        l2, li = oracle.errors_1d(nx, nt, dt, dx, u)
+        assert l2 / nx <= 1e-6, (nx, nt, eps, l2)
+        assert np.isfinite(u).all()
+
+
+def test_oracle_1d_restatement_small(oracle):
+    """The C restatement against a direct pure-Python transcription of
+    sum_local / sum_local_test / do_work (1d :186-224) on a small case."""
+    import math
+    nx, nt, eps, k, dt, dx = 13, 7, 3, 1.0, 0.001, 0.02
+    c = float(int((k * 3) / (pow(eps * dx, 3))))
+
+    def w(pos, t):
+        return math.cos(2 * math.pi * (t * dt)) * math.sin(2 * math.pi * (pos * dx))
+
+    S = [[math.sin(2 * math.pi * (x * dx)) for x in range(nx)], [0.0] * nx]
+    for t in range(nt):
+        cur, nxt = S[t % 2], S[(t + 1) % 2]
+        for x in range(nx):
+            r = 0.0
+            for sx in range(x - eps, x + eps + 1):
+                r += 1.0 * c * ((cur[sx] if 0 <= sx < nx else 0.0) - cur[x]) * dx
+            nxt[x] = cur[x] + (r * dt)
+            r2 = -(2 * math.pi * math.sin(2 * math.pi * (t * dt)) * math.sin(2 * math.pi * (x * dx)))
+            wp = w(x, t)
+            for sx in range(x - eps, x + eps + 1):
+                r2 -= 1.0 * c * ((w(sx, t) if 0 <= sx < nx else 0.0) - wp) * dx
+            nxt[x] += r2 * dt
+    u = oracle.run_1d(nx, nt, eps, k, dt, dx, True)
+    assert u.tolist() == S[nt % 2]
