@@ -161,10 +161,15 @@ typedef struct nlh_info {
 int nlh_get_info(const nlh_solver *s, nlh_info *info);
 
 /* Stencil-kernel timing with HIP events recorded on the stream the stencil
- * kernels are launched on.  While enabled, every nlh_run call is bracketed
- * by one event pair (its passes run back to back in between; a pass advances
- * nlh_info.steps_per_pass time steps); nlh_kernel_time returns the summed
- * duration and the number of time steps advanced since the last enable.   */
+ * kernels are launched on.  enable == 1: every nlh_run call is bracketed by
+ * one event pair on the interior stream (its passes run back to back in
+ * between; a pass advances nlh_info.steps_per_pass time steps).  enable == 2
+ * (busy time, the load balancer's input): an event pair around every stencil
+ * launch group on the stream that runs it (interior and edge bands), so
+ * halo waits are not counted -- the GPU counterpart of the reference's busy
+ * rate, 10000 - idle-rate (src/2d_nonlocal_distributed.cpp:112-128,855-860).
+ * nlh_kernel_time returns the summed duration and the number of time steps
+ * advanced since the last enable.                                          */
 int nlh_kernel_timing(nlh_solver *s, int enable);
 int nlh_kernel_time(nlh_solver *s, double *total_ms, int64_t *steps);
 
@@ -172,6 +177,40 @@ int nlh_kernel_time(nlh_solver *s, double *total_ms, int64_t *steps);
  * library (reference locidx(), src/2d_nonlocal_distributed.cpp:105-110).  */
 int nlh_resolve_owner(int64_t tiles_x, int64_t tiles_y, int32_t nranks,
                       const int32_t *owner_in, int32_t *owner_out);
+
+/* ---- load balancing (src/2d_nonlocal_distributed.cpp:844-959, 1306-1309) --
+ * Host-only policy replacing load_balance's work_realloc + DFS/BFS: busy[r]
+ * is rank r's busy time over one window.  Quota per rank as the reference
+ * (:905-927): d = mean - busy[r], tpt = busy[r]/tiles(r); ceil(d/tpt) if
+ * d > 0.3 tpt, floor(d/tpt) if -d > 0.3 tpt, else 0.  Whole tiles then move
+ * from negative- to positive-quota ranks, a donor never giving up its last
+ * tile, preferring tiles that border the receiver's region, and only when
+ * the move lowers the larger of the two ranks' predicted times (deterministic,
+ * so every rank derives the same map).  Returns the number of tiles moved
+ * (>= 0) or a negative NLH_ERR_* code.                                     */
+int nlh_balance_owner(int64_t tiles_x, int64_t tiles_y, int32_t nranks, const int32_t *owner,
+                      const double *busy, int32_t *owner_out);
+
+/* Collective: move to a new tile -> rank map (tiles_x*tiles_y entries, as
+ * nlh_params.owner).  Tiles whose owner changes travel over RCCL (ncclSend /
+ * ncclRecv of their interiors, nothing else); blocks, halo plan and exchange
+ * schedule are rebuilt; the field, the step index and the communicator are
+ * kept.  Replaces load_balance's reassignment of partition_space components
+ * (:937-944).  No snapshot may be in flight.                               */
+int nlh_repartition(nlh_solver *s, const int32_t *owner);
+
+/* Collective: one load-balancing round (the reference calls load_balance
+ * after step t when t % nbalance == 0, :1306-1309).  busy time per rank is
+ * this rank's stencil time since busy timing was enabled (nlh_kernel_timing
+ * (s, 2)), all-gathered over RCCL, or busy_in[nranks] when non-NULL (with
+ * NLH_VIRTUAL_RANKS one GPU runs every owner: the measured time is
+ * apportioned by owned tiles, nranks = the virtual count).  apply != 0:
+ * nlh_balance_owner picks the map and nlh_repartition applies it, and busy
+ * timing restarts.  owner_out (tiles_x*tiles_y) and busy_out (nranks), both
+ * optional, receive the resulting map and the busy times used.  Returns the
+ * number of tiles moved (>= 0) or a negative NLH_ERR_* code.              */
+int nlh_rebalance(nlh_solver *s, const double *busy_in, int32_t apply, int32_t *owner_out,
+                  double *busy_out);
 
 /* Host-only halo plan, for tests of the decomposition: number of halo
  * pieces this rank receives per pass (halo width: the one nlh_create resolves
@@ -189,13 +228,13 @@ int64_t nlh_halo_plan(const nlh_params *p, int64_t *pieces, int64_t cap);
 int64_t nlh_block_plan(const nlh_params *p, int64_t *blocks, int64_t cap);
 
 /* ---- 1D solver: drop-in for src/1d_nonlocal_serial.cpp --------------------
- *   nlh1d_create      solver::solver(nx, nt, eps, nlog)   1d :54-87
+ *   nlh1d_create      solver::solver(nx, nt, eps, nlog)   1d :69-89
  *                     (c_1d = (long)((k*3)/pow(eps*dx,3)), `long` in the
- *                      reference, :49,57 -- truncation kept)
- *   nlh1d_init_test   test_init()                         1d :127-132
- *   nlh1d_set_field   input_init()                        1d :119-125
- *   nlh1d_run         do_work() time loop                 1d :237-262
- *                     (sum_local :226-234, sum_local_test :214-223)
+ *                      reference, :57,74 -- truncation kept)
+ *   nlh1d_init_test   test_init()                         1d :124-129
+ *   nlh1d_set_field   input_init()                        1d :116-121
+ *   nlh1d_run         do_work() time loop                 1d :209-236
+ *                     (sum_local :198-206, sum_local_test :186-195)
  *   nlh1d_errors      compute_l2 / compute_linf           1d :91-103
  * One thread per node, the reference's per-term order (bitwise); the 1D
  * problem is small (the reference's batch rows have <= 1000 nodes).       */

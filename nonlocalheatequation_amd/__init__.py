@@ -30,7 +30,7 @@ import numpy as np
 __all__ = [
     "KERNEL_AUTO", "KERNEL_EXACT", "KERNEL_FAST", "INFLUENCE_CONSTANT", "INFLUENCE_LINEAR", "NLHError", "Solver",
     "lib", "lib_path", "comm_unique_id", "resolve_owner", "halo_plan", "block_plan",
-    "disk_count", "batch_tester", "BatchRow", "Solver1D", "batch_tester_1d",
+    "disk_count", "batch_tester", "BatchRow", "Solver1D", "batch_tester_1d", "balance_owner",
 ]
 
 KERNEL_AUTO, KERNEL_EXACT, KERNEL_FAST = 0, 1, 2
@@ -110,6 +110,11 @@ _SIGNATURES = {
                       ctypes.c_int64),
     "nlh_block_plan": ([ctypes.POINTER(_Params), ctypes.POINTER(ctypes.c_int64), ctypes.c_int64],
                        ctypes.c_int64),
+    "nlh_balance_owner": ([ctypes.c_int64, ctypes.c_int64, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32),
+                           ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
+    "nlh_repartition": ([ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
+    "nlh_rebalance": ([ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.c_int32,
+                       ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
     "nlh1d_create": ([ctypes.POINTER(_Params1D), ctypes.POINTER(ctypes.c_void_p)], ctypes.c_int),
     "nlh1d_destroy": ([ctypes.c_void_p], ctypes.c_int),
     "nlh1d_init_test": ([ctypes.c_void_p], ctypes.c_int),
@@ -226,6 +231,23 @@ def halo_plan(nx, ny, eps, tiles=(1, 1), owner=None, rank=0, nranks=1, split_til
     return out
 
 
+def balance_owner(tiles, nranks, owner, busy):
+    """Load-balance policy (nlh_balance_owner; replaces load_balance's
+    work_realloc + DFS/BFS, src/2d_nonlocal_distributed.cpp:844-959).
+    Returns (tiles moved, new owner map)."""
+    tx, ty = int(tiles[0]), int(tiles[1])
+    o = np.ascontiguousarray(owner, dtype=np.int32).reshape(-1)
+    b = np.ascontiguousarray(busy, dtype=np.float64).reshape(-1)
+    if o.size != tx * ty or b.size != nranks:
+        raise ValueError("owner needs tiles_x*tiles_y entries and busy nranks entries")
+    out = np.zeros(tx * ty, dtype=np.int32)
+    moved = lib().nlh_balance_owner(tx, ty, int(nranks), o.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                    _dp(b), out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
+    if moved < 0:
+        _check(-moved, "nlh_balance_owner")
+    return moved, out
+
+
 def disk_count(eps: int) -> int:
     """N(eps): lattice points of the closed disk, counted as the reference's
     loops do (len_1d_line, src/2d_nonlocal_serial.cpp:231,260-262)."""
@@ -273,6 +295,8 @@ class Solver:
         _check(lib().nlh_create(ctypes.byref(p), ctypes.byref(h)), "nlh_create")
         del keep
         self._h = h
+        self._tiles = (int(tiles[0]), int(tiles[1]))
+        self._nranks = int(nranks)
 
     # -- lifetime --------------------------------------------------------
     def close(self) -> None:
@@ -378,8 +402,33 @@ class Solver:
                     i.halo_bytes_sent, i.device_bytes, i.arch.decode(), i.halo_width, i.steps_per_pass,
                     i.pass_kernel.decode())
 
-    def kernel_timing(self, enable: bool) -> None:
-        _check(lib().nlh_kernel_timing(self._h, int(bool(enable))), "nlh_kernel_timing")
+    def kernel_timing(self, enable) -> None:
+        """False/0 off; True/1 one event pair per run(); 2 busy time (every
+        stencil launch group, halo waits excluded: the balancer's input)."""
+        _check(lib().nlh_kernel_timing(self._h, 2 if enable == 2 else int(bool(enable))), "nlh_kernel_timing")
+
+    def repartition(self, owner) -> None:
+        """Collective: move tiles to a new tile -> rank map (index gx + gy*tx);
+        field and step index are kept."""
+        o = np.ascontiguousarray(owner, dtype=np.int32).reshape(-1)
+        _check(lib().nlh_repartition(self._h, o.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))), "nlh_repartition")
+
+    def rebalance(self, busy=None, apply=True, nowners=None):
+        """Collective load-balancing round (load_balance, :1306-1309): busy
+        times measured with kernel_timing(2) (or ``busy``, one per owner), the
+        policy's map applied.  Returns (tiles moved, owner map, busy used)."""
+        ntiles = self._tiles[0] * self._tiles[1]
+        nown = int(nowners or (len(busy) if busy is not None else self._nranks))
+        out = np.zeros(ntiles, dtype=np.int32)
+        bo = np.zeros(nown, dtype=np.float64)
+        bi = None
+        if busy is not None:
+            bi = np.ascontiguousarray(busy, dtype=np.float64)
+        rc = lib().nlh_rebalance(self._h, _dp(bi) if bi is not None else None, int(bool(apply)),
+                                 out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), _dp(bo))
+        if rc < 0:
+            _check(-rc, "nlh_rebalance")
+        return rc, out, bo
 
     def kernel_time(self):
         """(summed stencil-pass milliseconds, time steps those passes advanced)."""

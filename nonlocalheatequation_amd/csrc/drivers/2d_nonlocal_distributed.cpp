@@ -10,10 +10,17 @@
 // exchanges only eps-wide ghost strips with RCCL send/recv over xGMI,
 // overlapped with the interior kernel.  Rank 0 prints, as locality 0 does.
 // Flags/defaults (:1415-1458), batch format (:1328-1359), outputs (:522-560,
-// :1408-1409) as the reference.  --nbalance / --test_load_balance are accepted;
-// the decomposition is static (dynamic load balancing, :844-959, is out of
-// scope).  Extra flags --kernel auto|exact|fast, --device N.
+// :1408-1409) as the reference.  --nbalance N: after every step t with
+// t % N == 0 (t != 0, several ranks; :1306-1309) the ranks all-gather their
+// measured busy time (stencil-kernel time, HIP events; the reference uses the
+// HPX idle-rate counter) and move whole tiles to even it out (nlh_rebalance).
+// --test_load_balance prints the busy rates, the tile map and whether the
+// spread is within the reference's bound (:647-686).  Extra flags --kernel
+// auto|exact|fast, --device N.
+#include <algorithm>
+#include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <iostream>
 #include <string>
 #include <vector>
@@ -31,6 +38,14 @@ struct Run {
   bool test;
   std::vector<int32_t> owner;  // empty: locidx() default
 };
+
+// owners in the tile map: the ranks, or NLH_VIRTUAL_RANKS on one rank
+// (diagnostics: every owner on one GPU, busy time apportioned by tiles)
+static int owners_of(const RankEnv &re) {
+  if (const char *v = std::getenv("NLH_VIRTUAL_RANKS"))
+    if (re.nranks == 1 && std::atoi(v) > 1) return std::atoi(v);
+  return re.nranks;
+}
 
 static int make_solver(const Run &r, const RankEnv &re, const uint8_t *id, int kernel, int device,
                        nlh_solver **out) {
@@ -51,7 +66,7 @@ static int make_solver(const Run &r, const RankEnv &re, const uint8_t *id, int k
   p.tiles_y = r.npy;
   std::vector<int32_t> own = r.owner;
   for (auto &v : own)
-    if (v >= re.nranks) v %= re.nranks;  // a map written for more localities than ranks
+    if (v >= owners_of(re)) v %= owners_of(re);  // a map written for more localities than ranks
   p.owner = own.empty() ? nullptr : own.data();
   p.comm_id = re.nranks > 1 ? id : nullptr;
   if (nlh_create(&p, out) != NLH_OK) return die("nlh_create");
@@ -165,11 +180,54 @@ int main(int argc, char **argv) {
   Logger lg;
   lg.nx = gx, lg.ny = gy, lg.dt = r.dt, lg.dh = r.dh, lg.test = r.test;
   lg.probe();
+  // dynamic load balancing (several ranks only, as the reference's nl > 1)
+  const uint64_t nbal_u = o.as_u64("nbalance");
+  const int64_t nbalance = nbal_u >= (uint64_t)INT64_MAX ? 0 : (int64_t)nbal_u;
+  const int owners = owners_of(re);
+  const bool balancing = owners > 1 && nbalance > 0 && nbalance < r.nt;
+  const bool lb_test = o.count("test_load_balance") != 0;
+  const int64_t ntiles = r.npx * r.npy;
+  std::vector<int32_t> map(ntiles, 0);
+  std::vector<double> busy(owners, 0.0);
+  uint64_t window0 = 0;  // start of the current busy window (host clock)
+  if ((balancing || lb_test) && nlh_kernel_timing(s, 2) != NLH_OK) return die("nlh_kernel_timing");
+  auto on_balance = [&](int64_t) -> int {
+    const int rc = nlh_rebalance(s, nullptr, 1, map.data(), busy.data());
+    window0 = now_ns();
+    return rc < 0 ? -rc : NLH_OK;
+  };
   uint64_t elapsed = 0;
-  if (run_steps(s, r.nt, nlog, lg, true, re.rank, elapsed, re.nranks) != NLH_OK) return die("nlh_run");
+  window0 = now_ns();
+  if (run_steps(s, r.nt, nlog, lg, true, re.rank, elapsed, re.nranks, balancing ? nbalance : 0,
+                balancing ? std::function<int(int64_t)>(on_balance) : std::function<int(int64_t)>()) != NLH_OK)
+    return die("nlh_run");
 
-  if (o.count("test_load_balance") && re.rank == 0)
-    std::cerr << "[note] static block decomposition: no dynamic load balancing to test" << std::endl;
+  if (lb_test) {
+    // busy rate in the reference's units (10000 = busy the whole window):
+    // stencil time since the last rebalance over that window's wall time
+    const double window_ms = std::max(1e-9, (now_ns() - window0) / 1e6);
+    const int rc = nlh_rebalance(s, nullptr, 0, map.data(), busy.data());
+    if (rc < 0) return die("nlh_rebalance");
+    if (re.rank == 0) {
+      std::cout << "Testing load balance:" << std::endl;
+      double expected = 0.0, max_diff = 0.0;
+      std::vector<double> rate(owners);
+      for (int i = 0; i < owners; ++i) {
+        rate[i] = std::min(10000.0, 10000.0 * busy[i] / window_ms);
+        std::cout << "Test: counter value: " << rate[i] << std::endl;
+        expected += rate[i];
+      }
+      expected /= owners;
+      std::cout << "Expected busy rate " << expected << std::endl;
+      for (int i = 0; i < owners; ++i) max_diff = std::max(std::abs(expected - rate[i]), max_diff);
+      std::cout << "Visualizing Load Balance across nodes" << std::endl;
+      for (int64_t ix = 0; ix < r.npx; ++ix) {
+        for (int64_t iy = 0; iy < r.npy; ++iy) std::cout << map[ix + iy * r.npx] << " ";
+        std::cout << std::endl;
+      }
+      std::cout << (max_diff > 1500 ? "Load not balanced correctly" : "Load balanced correctly") << std::endl;
+    }
+  }
 
   std::vector<double> u;
   if ((r.test && o.as_bool("cmp")) || o.count("results")) {

@@ -16,6 +16,7 @@
 #include <cstring>
 #include <ctime>
 #include <fstream>
+#include <functional>
 #include <iostream>
 #include <thread>
 
@@ -297,7 +298,8 @@ void Logger::log(int64_t t, int64_t vtk_index, const std::vector<double> &u) {
 
 // ---------------------------------------------------------------- loop
 int run_steps(nlh_solver *s, int64_t nt, int64_t nlog, Logger &lg, bool vtk_index_is_t,
-              int rank, uint64_t &elapsed_ns, int nranks) {
+              int rank, uint64_t &elapsed_ns, int nranks, int64_t nbalance,
+              const std::function<int(int64_t)> &on_balance) {
   const bool logging = lg.enabled() && nlog > 0;
   // one rank: log steps take an asynchronous snapshot (device copy in stream
   // order, host transfer on a copy stream) and a writer thread formats the
@@ -321,8 +323,18 @@ int run_steps(nlh_solver *s, int64_t nt, int64_t nlog, Logger &lg, bool vtk_inde
       const int64_t next_log = (t % nlog == 0) ? t : (t / nlog + 1) * nlog;
       last = std::min(last, next_log);
     }
+    const bool balancing = nbalance > 0 && on_balance;
+    if (balancing) {  // load_balance after step t when t % nbalance == 0, t != 0 (:1306)
+      const int64_t from = std::max<int64_t>(t, 1);
+      const int64_t next_bal = (from % nbalance == 0) ? from : (from / nbalance + 1) * nbalance;
+      last = std::min(last, next_bal);
+    }
     if ((rc = nlh_run(s, last - t + 1)) != NLH_OK) break;
     t = last + 1;
+    if (balancing && last != 0 && last % nbalance == 0) {
+      if ((rc = join_writer()) != NLH_OK) break;  // no snapshot across a repartition
+      if ((rc = on_balance(last)) != NLH_OK) break;
+    }
     if (logging && last % nlog == 0) {
       const int64_t vi = vtk_index_is_t ? last : last / nlog;
       if (async_log) {

@@ -13,6 +13,7 @@
 //   CSV logging (src/2d_nonlocal_serial.cpp:149-177, async :214-284)
 #pragma once
 #include <cstdint>
+#include <functional>
 #include <map>
 #include <string>
 #include <vector>
@@ -95,8 +96,12 @@ void print_errors(double l2, double linf);
 // and a writer thread writes the files while the following steps run.
 // Returns NLH_OK and the wall time of the loop (all ranks finished, the last
 // files written) in elapsed_ns.
+// nbalance > 0: on_balance(t) runs after step t whenever t % nbalance == 0
+// and t != 0 (the reference's load_balance cadence, src/2d_nonlocal_
+// distributed.cpp:1306-1309), before that step's log.
 int run_steps(nlh_solver *s, int64_t nt, int64_t nlog, Logger &lg, bool vtk_index_is_t,
-              int rank, uint64_t &elapsed_ns, int nranks = 1);
+              int rank, uint64_t &elapsed_ns, int nranks = 1, int64_t nbalance = 0,
+              const std::function<int(int64_t)> &on_balance = {});
 
 // Read the reference's --file partition file (src/2d_nonlocal_distributed.cpp:
 // 467-488): "nx ny npx npy dh" then npx*npy lines "px py owner", px outer.

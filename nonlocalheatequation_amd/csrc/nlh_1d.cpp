@@ -1,7 +1,7 @@
 // nlh_1d.cpp -- C ABI of the 1D solver (include/nlh.h, nlh1d_*): the
 // drop-in for the reference's src/1d_nonlocal_serial.cpp.  Device field of
 // nx + 2 eps doubles whose eps-wide frames stay 0 (the reference's
-// boundary(), 1d :203-208); one launch of k_1d (nlh_kernels.hip) per step.
+// boundary(), 1d :178-183); one launch of k_1d (nlh_kernels.hip) per step.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -72,7 +72,7 @@ int create1d(const nlh1d_params &p, nlh1d_solver *s) {
   HIP1D(hipGetDeviceProperties(&prop, s->device));
   if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
     return fail1d(NLH_ERR_UNSUPPORTED, std::string("libnlh is built for gfx950, device is ") + prop.gcnArchName);
-  // the reference's `long c_1d` (1d :49,57): truncated toward zero
+  // the reference's `long c_1d` (1d :57,74): truncated toward zero
   s->c1d = (double)(long)((p.k * 3) / (pow(p.eps * p.dx, 3)));
   const int64_t n = p.nx + 2 * p.eps;
   for (auto &b : s->base) {
@@ -115,7 +115,7 @@ int nlh1d_destroy(nlh1d_solver *s) {
 int nlh1d_init_test(nlh1d_solver *s) {
   if (!s) return fail1d(NLH_ERR_ARG, "null solver");
   HIP1D(hipSetDevice(s->device));
-  // u(x, 0) = sin(2 pi (x dx)) = the table's interior (1d :127-132)
+  // u(x, 0) = sin(2 pi (x dx)) = the table's interior (1d :124-129)
   HIP1D(hipMemcpyAsync(s->base[0] + s->p.eps, s->d_sxt + s->p.eps, s->p.nx * sizeof(double),
                        hipMemcpyDeviceToDevice, s->st));
   HIP1D(hipStreamSynchronize(s->st));
@@ -146,7 +146,7 @@ int nlh1d_run(nlh1d_solver *s, int64_t nsteps) {
   if (nsteps < 0) return fail1d(NLH_ERR_ARG, "negative step count");
   HIP1D(hipSetDevice(s->device));
   for (int64_t i = 0; i < nsteps; ++i) {
-    // (2*M_PI)*(time*dt) as the reference spells it (1d :215, :184)
+    // (2*M_PI)*(time*dt) as the reference spells it (1d :174, :187)
     const double arg = 2 * M_PI * (s->t * s->p.dt);
     const int rc = nlh::launch_1d(s->base[s->cur] + s->p.eps, s->base[1 - s->cur] + s->p.eps, s->p.nx,
                                   (int32_t)s->p.eps, s->c1d, s->p.dt, s->p.dx, s->p.test != 0,

@@ -149,6 +149,23 @@ struct LocalBlock {
   bool L = false, Rr = false, T = false, B = false;
 };
 
+// std::atomic<bool> that copies by value, so a rebuilt solver can be moved
+// into the caller's handle (nlh_repartition)
+struct Flag {
+  std::atomic<bool> v{false};
+  Flag() = default;
+  Flag(const Flag &o) : v(o.v.load()) {}
+  Flag &operator=(const Flag &o) {
+    v = o.v.load();
+    return *this;
+  }
+  Flag &operator=(bool b) {
+    v = b;
+    return *this;
+  }
+  operator bool() const { return v.load(); }
+};
+
 struct Peer {
   int rank = 0;
   int64_t send_count = 0, recv_count = 0;  // doubles
@@ -183,6 +200,7 @@ struct nlh_solver {
   // NLH_VIRTUAL_RANKS: per plan piece, 1 if it crosses virtual owners (goes
   // over RCCL to self); empty otherwise
   std::vector<uint8_t> vremote;
+  int owners = 1;  // owner ids in the tile map: nranks, or NLH_VIRTUAL_RANKS
   // exchange schedule (profiles/r01/sched): interior workgroups per CU in the
   // segment model when an exchange runs beside it (RCCL kernels need the LDS
   // a fourth k_pair_split workgroup would hold; NLH_INT_PER_CU, 0 = all), and
@@ -210,8 +228,8 @@ struct nlh_solver {
   std::vector<int> part_off;
   int part_total = 0;
   double *d_red = nullptr;
-  // timing
-  bool timing = false;
+  // timing: 0 off, 1 one event pair per nlh_run, 2 busy (a pair per launch group)
+  int timing = 0;
   std::vector<hipEvent_t> ev_pool;
   size_t ev_used = 0;
   std::vector<int> ev_steps;  // time steps covered by each timed event pair
@@ -222,7 +240,7 @@ struct nlh_solver {
   hipStream_t s_copy = nullptr;
   hipEvent_t ev_snap_dev = nullptr, ev_snap = nullptr;
   double *snap_dev = nullptr, *snap_host = nullptr;
-  std::atomic<bool> snap_pending{false};
+  Flag snap_pending;
 };
 
 namespace {
@@ -575,7 +593,23 @@ int enqueue_step(nlh_solver *s, int nsteps) {
   const bool two = nsteps == 2;
   set_time(s, s->t);
   auto stencil = [&](const std::vector<nlh::RectList> &one, const std::vector<nlh::RectList> &pr,
-                     hipStream_t st) { return two ? launch_pair_lists(s, pr, st) : launch_stencil(s, one, st); };
+                     hipStream_t st) {
+    bool any = false;
+    for (const auto &rl : two ? pr : one) any |= rl.nwork > 0;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (s->timing == 2 && any) {  // busy time: this launch group only
+      e0 = pool_event(s);
+      e1 = pool_event(s);
+      if (!e0 || !e1) return fail(NLH_ERR_HIP, "event pool");
+      HIP_TRY(hipEventRecord(e0, st));
+    }
+    const int r = two ? launch_pair_lists(s, pr, st) : launch_stencil(s, one, st);
+    if (e1) {
+      HIP_TRY(hipEventRecord(e1, st));
+      s->ev_steps.push_back(st == s->s_main ? nsteps : 0);  // steps counted on the interior group
+    }
+    return r;
+  };
   int rc;
   if (!s->exchange) {
     if ((rc = stencil(s->rl_full[k], s->pl_full[k], s->s_main))) return rc;
@@ -652,14 +686,14 @@ int compute_lw(nlh_solver *s) {
   return NLH_OK;
 }
 
-int destroy_impl(nlh_solver *s) {
-  if (!s) return NLH_OK;
+// frees every device resource; the communicator too unless keep_comm
+void release_impl(nlh_solver *s, bool keep_comm) {
   (void)hipSetDevice(s->device);
   if (s->s_main) (void)hipStreamSynchronize(s->s_main);
   if (s->s_comm) (void)hipStreamSynchronize(s->s_comm);
   if (s->s_band) (void)hipStreamSynchronize(s->s_band);
   if (s->s_copy) (void)hipStreamSynchronize(s->s_copy);
-  if (s->comm) ncclCommDestroy(s->comm);
+  if (s->comm && !keep_comm) ncclCommDestroy(s->comm);
   (void)hipFree(s->snap_dev);
   if (s->snap_host) (void)hipHostFree(s->snap_host);
   if (s->ev_snap_dev) (void)hipEventDestroy(s->ev_snap_dev);
@@ -689,11 +723,17 @@ int destroy_impl(nlh_solver *s) {
   if (s->s_main) (void)hipStreamDestroy(s->s_main);
   if (s->s_comm) (void)hipStreamDestroy(s->s_comm);
   if (s->s_band) (void)hipStreamDestroy(s->s_band);
+}
+
+int destroy_impl(nlh_solver *s) {
+  if (!s) return NLH_OK;
+  release_impl(s, false);
   delete s;
   return NLH_OK;
 }
 
-int create_impl(const nlh_params *pin, nlh_solver *s) {
+// reuse_comm: an existing communicator over the same ranks (nlh_repartition)
+int create_impl(const nlh_params *pin, nlh_solver *s, ncclComm_t reuse_comm = nullptr) {
   const nlh_params &p = *pin;
   if (p.nx <= 0 || p.ny <= 0) return fail(NLH_ERR_ARG, "nx, ny must be positive");
   if (p.eps < 1) return fail(NLH_ERR_ARG, "eps must be >= 1");
@@ -711,6 +751,7 @@ int create_impl(const nlh_params *pin, nlh_solver *s) {
 
   std::string err;
   const int vranks = virtual_ranks(p);
+  s->owners = vranks ? vranks : p.nranks;
   if (!nlh::resolve_owner(tx, ty, vranks ? vranks : p.nranks, p.owner, s->owner, err))
     return fail(NLH_ERR_ARG, err);
 
@@ -876,7 +917,9 @@ int create_impl(const nlh_params *pin, nlh_solver *s) {
   if (s->pair && (rc = build_rectlists(s, 1))) return rc;
 
   // ---- RCCL communicator and exchange plan
-  if (p.nranks > 1) {
+  if (reuse_comm) {
+    s->comm = reuse_comm;
+  } else if (p.nranks > 1) {
     if (!p.comm_id) return fail(NLH_ERR_ARG, "nranks > 1 requires comm_id");
     ncclUniqueId id;
     static_assert(sizeof(ncclUniqueId) == NLH_COMM_ID_BYTES, "unique id size");
@@ -907,6 +950,148 @@ int create_impl(const nlh_params *pin, nlh_solver *s) {
     if (rc) return rc;
   }
   return NLH_OK;
+}
+
+// the plan block holding global node (x, y): its rank and local block index
+void locate(const nlh_solver *s, int64_t x, int64_t y, int &rank, int &local) {
+  rank = -1;
+  local = -1;
+  for (size_t b = 0; b < s->plan.blocks.size(); ++b) {
+    const nlh::GRect &r = s->plan.blocks[b].r;
+    if (x < r.x0 || x >= r.x0 + r.w || y < r.y0 || y >= r.y0 + r.h) continue;
+    rank = s->plan.blocks[b].rank;
+    for (size_t j = 0; j < s->blocks.size(); ++j)
+      if (s->blocks[j].plan_index == (int)b) local = (int)j;
+    return;
+  }
+}
+
+double *tile_ptr(const nlh_solver *s, int local, int k, int64_t x0, int64_t y0) {
+  const LocalBlock &b = s->blocks[local];
+  return b.origin(k) + (y0 - b.r.y0) * b.pitch + (x0 - b.r.x0);
+}
+
+// rebuild the solver for a new tile -> owner map, moving the tiles that
+// change rank over RCCL (src/2d_nonlocal_distributed.cpp:937-944)
+int repartition_impl(nlh_solver *s, const std::vector<int32_t> &own) {
+  if (s->snap_pending) return fail(NLH_ERR_STATE, "a snapshot is in flight (call nlh_snapshot_wait)");
+  int rc = set_device(s);
+  if (rc) return rc;
+  HIP_TRY(hipStreamSynchronize(s->s_main));
+  HIP_TRY(hipStreamSynchronize(s->s_comm));
+  HIP_TRY(hipStreamSynchronize(s->s_band));
+  if (own == s->owner) return NLH_OK;
+  nlh_params p = s->p;
+  p.owner = own.data();
+  p.comm_id = nullptr;
+  nlh_solver *n = new nlh_solver();
+  rc = create_impl(&p, n, s->comm);
+  if (rc) {
+    const std::string keep = g_err;
+    n->comm = nullptr;  // still the caller's
+    destroy_impl(n);
+    g_err = keep;
+    return rc;
+  }
+  const int me = (int)p.rank;
+  const int64_t tw = p.nx / p.tiles_x, th = p.ny / p.tiles_y;
+  struct Mv {
+    int64_t x0, y0;
+    int src, dst;  // local block indices in s (source) and n (destination)
+  };
+  std::vector<Mv> local;
+  std::map<int, std::vector<Mv>> sends, recvs;  // by peer rank, tile order
+  for (int64_t i = 0; i < p.tiles_x * p.tiles_y; ++i) {
+    const int64_t x0 = (i % p.tiles_x) * tw, y0 = (i / p.tiles_x) * th;
+    int ro, lo, rn, ln;
+    locate(s, x0, y0, ro, lo);
+    locate(n, x0, y0, rn, ln);
+    if (ro == me && rn == me) local.push_back({x0, y0, lo, ln});
+    else if (ro == me) sends[rn].push_back({x0, y0, lo, -1});
+    else if (rn == me) recvs[ro].push_back({x0, y0, -1, ln});
+  }
+  const size_t tb = (size_t)(tw * th);
+  const size_t pitch_b = (size_t)tw * sizeof(double);
+  int status = NLH_OK;
+  std::vector<double *> bufs;
+  auto stage = [&](size_t ntiles) -> double * {
+    double *b = nullptr;
+    if (hipMalloc(&b, std::max<size_t>(ntiles * tb, 1) * sizeof(double)) != hipSuccess) return nullptr;
+    bufs.push_back(b);
+    return b;
+  };
+  hipStream_t st = n->s_main;
+  for (const Mv &m : local) {
+    if (hipMemcpy2DAsync(tile_ptr(n, m.dst, 0, m.x0, m.y0), n->blocks[m.dst].pitch * sizeof(double),
+                         tile_ptr(s, m.src, s->cur, m.x0, m.y0), s->blocks[m.src].pitch * sizeof(double),
+                         pitch_b, th, hipMemcpyDeviceToDevice, st) != hipSuccess)
+      status = fail(NLH_ERR_HIP, "repartition local copy");
+  }
+  std::map<int, double *> sbuf, rbuf;
+  for (auto &kv : sends) {
+    double *b = stage(kv.second.size());
+    if (!b) { status = fail(NLH_ERR_HIP, "repartition staging"); break; }
+    sbuf[kv.first] = b;
+    for (size_t j = 0; j < kv.second.size() && status == NLH_OK; ++j) {
+      const Mv &m = kv.second[j];
+      if (hipMemcpy2DAsync(b + j * tb, pitch_b, tile_ptr(s, m.src, s->cur, m.x0, m.y0),
+                           s->blocks[m.src].pitch * sizeof(double), pitch_b, th, hipMemcpyDeviceToDevice,
+                           st) != hipSuccess)
+        status = fail(NLH_ERR_HIP, "repartition pack");
+    }
+  }
+  for (auto &kv : recvs) {
+    if (status != NLH_OK) break;
+    double *b = stage(kv.second.size());
+    if (!b) { status = fail(NLH_ERR_HIP, "repartition staging"); break; }
+    rbuf[kv.first] = b;
+  }
+  if (status == NLH_OK && (!sends.empty() || !recvs.empty())) {
+    if (!n->comm) {
+      status = fail(NLH_ERR_STATE, "internal: tiles change rank without a communicator");
+    } else {
+      bool ok = ncclGroupStart() == ncclSuccess;
+      for (auto &kv : sends)
+        ok = ok && ncclSend(sbuf[kv.first], kv.second.size() * tb, ncclDouble, kv.first, n->comm, st) == ncclSuccess;
+      for (auto &kv : recvs)
+        ok = ok && ncclRecv(rbuf[kv.first], kv.second.size() * tb, ncclDouble, kv.first, n->comm, st) == ncclSuccess;
+      ok = (ncclGroupEnd() == ncclSuccess) && ok;
+      if (!ok) status = fail(NLH_ERR_RCCL, "repartition send/recv");
+    }
+  }
+  for (auto &kv : recvs) {
+    if (status != NLH_OK) break;
+    for (size_t j = 0; j < kv.second.size(); ++j) {
+      const Mv &m = kv.second[j];
+      if (hipMemcpy2DAsync(tile_ptr(n, m.dst, 0, m.x0, m.y0), n->blocks[m.dst].pitch * sizeof(double),
+                           rbuf[kv.first] + j * tb, pitch_b, pitch_b, th, hipMemcpyDeviceToDevice,
+                           st) != hipSuccess)
+        status = fail(NLH_ERR_HIP, "repartition unpack");
+    }
+  }
+  if (hipStreamSynchronize(st) != hipSuccess && status == NLH_OK) status = fail(NLH_ERR_HIP, "repartition sync");
+  for (double *b : bufs) (void)hipFree(b);
+  if (status != NLH_OK) {
+    const std::string keep = g_err;
+    n->comm = nullptr;
+    destroy_impl(n);
+    g_err = keep;
+    return status;
+  }
+  n->t = s->t;
+  n->cur = 0;
+  n->halo_fresh = false;
+  n->timing = s->timing;
+  release_impl(s, true);  // the communicator lives on in n
+  *s = std::move(*n);
+  delete n;  // moved-from shell: its resources now belong to s
+  return NLH_OK;
+}
+
+// this rank's busy milliseconds since busy timing was enabled
+int local_busy(nlh_solver *s, double &ms) {
+  int64_t steps = 0;
+  return nlh_kernel_time(s, &ms, &steps);
 }
 
 }  // namespace
@@ -1117,7 +1302,7 @@ int nlh_run(nlh_solver *s, int64_t nsteps) {
   // timing: one event pair on the stencil stream around the whole call, so
   // back-to-back passes are not separated by per-launch event records
   hipEvent_t e0 = nullptr, e1 = nullptr;
-  if (s->timing) {
+  if (s->timing == 1) {
     e0 = pool_event(s);
     e1 = pool_event(s);
     if (!e0 || !e1) return fail(NLH_ERR_HIP, "event pool");
@@ -1217,7 +1402,9 @@ int nlh_kernel_timing(nlh_solver *s, int enable) {
   int rc = set_device(s);
   if (rc) return rc;
   HIP_TRY(hipStreamSynchronize(s->s_main));
-  s->timing = enable != 0;
+  HIP_TRY(hipStreamSynchronize(s->s_comm));
+  HIP_TRY(hipStreamSynchronize(s->s_band));
+  s->timing = enable == 2 ? 2 : enable != 0 ? 1 : 0;
   s->ev_used = 0;
   s->ev_steps.clear();
   return NLH_OK;
@@ -1228,6 +1415,8 @@ int nlh_kernel_time(nlh_solver *s, double *total_ms, int64_t *steps_out) {
   int rc = set_device(s);
   if (rc) return rc;
   HIP_TRY(hipStreamSynchronize(s->s_main));
+  HIP_TRY(hipStreamSynchronize(s->s_comm));
+  HIP_TRY(hipStreamSynchronize(s->s_band));
   double tot = 0.0;
   for (size_t i = 0; i + 1 < s->ev_used; i += 2) {
     float ms = 0.f;
@@ -1310,6 +1499,79 @@ int64_t nlh_block_plan(const nlh_params *p, int64_t *blocks, int64_t cap) {
     ++n;
   }
   return n;
+}
+
+int nlh_balance_owner(int64_t tiles_x, int64_t tiles_y, int32_t nranks, const int32_t *owner,
+                      const double *busy, int32_t *owner_out) {
+  if (tiles_x < 1 || tiles_y < 1 || nranks < 1 || !owner || !busy || !owner_out)
+    return -fail(NLH_ERR_ARG, "bad argument");
+  std::vector<int32_t> o, out;
+  std::string err;
+  if (!nlh::resolve_owner(tiles_x, tiles_y, nranks, owner, o, err)) return -fail(NLH_ERR_ARG, err);
+  for (int r = 0; r < nranks; ++r)
+    if (!(busy[r] >= 0.0)) return -fail(NLH_ERR_ARG, "busy times must be finite and >= 0");
+  const int moved = nlh::balance_owner(tiles_x, tiles_y, nranks, o, busy, out);
+  std::memcpy(owner_out, out.data(), out.size() * sizeof(int32_t));
+  return moved;
+}
+
+int nlh_repartition(nlh_solver *s, const int32_t *owner) {
+  if (!s || !owner) return fail(NLH_ERR_ARG, "null argument");
+  std::vector<int32_t> o;
+  std::string err;
+  if (!nlh::resolve_owner(s->p.tiles_x, s->p.tiles_y, s->owners, owner, o, err)) return fail(NLH_ERR_ARG, err);
+  return repartition_impl(s, o);
+}
+
+int nlh_rebalance(nlh_solver *s, const double *busy_in, int32_t apply, int32_t *owner_out,
+                  double *busy_out) {
+  if (!s) return -fail(NLH_ERR_ARG, "null solver");
+  int rc = set_device(s);
+  if (rc) return -rc;
+  const int R = s->owners;
+  std::vector<double> busy(R, 0.0);
+  if (busy_in) {
+    for (int r = 0; r < R; ++r) busy[r] = busy_in[r];
+  } else {
+    if (s->timing != 2) return -fail(NLH_ERR_STATE, "busy timing is off (nlh_kernel_timing(s, 2))");
+    double mine = 0.0;
+    if ((rc = local_busy(s, mine))) return -rc;
+    if (R != s->p.nranks) {
+      // NLH_VIRTUAL_RANKS: one GPU runs every owner; its measured busy time
+      // is apportioned by owned tiles (tiles are equal-sized)
+      std::vector<int64_t> cnt(R, 0);
+      for (int32_t v : s->owner) ++cnt[v];
+      for (int r = 0; r < R; ++r) busy[r] = mine * (double)cnt[r] / (double)s->owner.size();
+    } else {
+      busy[s->p.rank] = mine;
+    }
+    if (s->comm && R > 1 && R == s->p.nranks) {
+      double *d = nullptr;
+      if (hipMalloc(&d, (R + 1) * sizeof(double)) != hipSuccess) return -fail(NLH_ERR_HIP, "busy buffer");
+      int st = NLH_OK;
+      if (hipMemcpyAsync(d + R, &mine, sizeof(double), hipMemcpyHostToDevice, s->s_comm) != hipSuccess)
+        st = fail(NLH_ERR_HIP, "busy upload");
+      if (st == NLH_OK && ncclAllGather(d + R, d, 1, ncclDouble, s->comm, s->s_comm) != ncclSuccess)
+        st = fail(NLH_ERR_RCCL, "busy all-gather");
+      if (st == NLH_OK && hipMemcpyAsync(busy.data(), d, R * sizeof(double), hipMemcpyDeviceToHost, s->s_comm) != hipSuccess)
+        st = fail(NLH_ERR_HIP, "busy download");
+      if (hipStreamSynchronize(s->s_comm) != hipSuccess && st == NLH_OK) st = fail(NLH_ERR_HIP, "busy sync");
+      (void)hipFree(d);
+      if (st) return -st;
+    }
+  }
+  if (busy_out) std::memcpy(busy_out, busy.data(), R * sizeof(double));
+  int moved = 0;
+  if (apply) {
+    for (int r = 0; r < R; ++r)
+      if (!(busy[r] >= 0.0)) return -fail(NLH_ERR_ARG, "busy times must be finite and >= 0");
+    std::vector<int32_t> next;
+    moved = nlh::balance_owner(s->p.tiles_x, s->p.tiles_y, R, s->owner, busy.data(), next);
+    if (moved > 0 && (rc = repartition_impl(s, next))) return -rc;
+    if (s->timing == 2 && (rc = nlh_kernel_timing(s, 2))) return -rc;  // a new busy window
+  }
+  if (owner_out) std::memcpy(owner_out, s->owner.data(), s->owner.size() * sizeof(int32_t));
+  return moved;
 }
 
 }  // extern "C"

@@ -175,10 +175,10 @@ __global__ __launch_bounds__(256) void k_1d(const double *u, double *un, int64_t
   const int64_t x = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (x >= nx) return;
   const double ui = u[x];
-  double res = 0.0;  // sum_local (1d :226-234)
+  double res = 0.0;  // sum_local (1d :198-206)
   for (int d = -eps; d <= eps; ++d) res += ((1.0 * c) * (u[x + d] - ui)) * dx;
   double out = ui + (res * dt);
-  if (TEST) {  // sum_local_test (1d :214-223), w from the host sin table
+  if (TEST) {  // sum_local_test (1d :186-195), w from the host sin table
     double r2 = -(st2pi * sxt[x + eps]);
     const double wpos = ct * sxt[x + eps];
     for (int d = -eps; d <= eps; ++d) {

@@ -2,6 +2,8 @@
 #include "nlh_plan.h"
 
 #include <algorithm>
+#include <cmath>
+#include <cstdlib>
 
 namespace nlh {
 
@@ -106,6 +108,106 @@ Plan make_plan(int64_t nx, int64_t ny, int64_t eps, int64_t tiles_x,
     }
   }
   return plan;
+}
+
+int balance_owner(int64_t tiles_x, int64_t tiles_y, int32_t nranks,
+                  const std::vector<int32_t> &owner, const double *busy,
+                  std::vector<int32_t> &owner_out) {
+  const int64_t T = tiles_x * tiles_y;
+  owner_out = owner;
+  if (nranks < 2 || T < 2) return 0;
+  std::vector<int64_t> n(nranks, 0);
+  for (int64_t i = 0; i < T; ++i) ++n[owner[i]];
+  double total = 0.0;
+  for (int r = 0; r < nranks; ++r) total += busy[r] > 0 ? busy[r] : 0.0;
+  if (!(total > 0.0)) return 0;
+  const double mean = total / nranks;
+  // quota per rank, the reference's work_realloc (:905-927); a rank without
+  // tiles is priced at the job's mean time per tile
+  std::vector<int64_t> w(nranks, 0);
+  std::vector<double> P(nranks), tp(nranks);  // predicted busy time, time per tile
+  for (int r = 0; r < nranks; ++r) {
+    const double b = busy[r] > 0 ? busy[r] : 0.0;
+    const double tpt = n[r] > 0 && b > 0 ? b / (double)n[r] : total / (double)T;
+    P[r] = b;
+    tp[r] = tpt;
+    const double d = mean - b;
+    if (d > 0 && d > 0.3 * tpt)
+      w[r] = (int64_t)std::ceil(d / tpt);
+    else if (d < 0 && -d > 0.3 * tpt)
+      w[r] = (int64_t)std::floor(d / tpt);
+  }
+  std::vector<int32_t> &o = owner_out;
+  auto nbrs = [&](int64_t t, int64_t out[4]) {
+    const int64_t gx = t % tiles_x, gy = t / tiles_x;
+    int k = 0;
+    if (gx > 0) out[k++] = t - 1;
+    if (gx + 1 < tiles_x) out[k++] = t + 1;
+    if (gy > 0) out[k++] = t - tiles_x;
+    if (gy + 1 < tiles_y) out[k++] = t + tiles_x;
+    return k;
+  };
+  int moved = 0;
+  for (int64_t guard = 0; guard < T * nranks; ++guard) {
+    // adjacent moves: (quota gap, receiver-owned neighbours, -tile index)
+    int64_t bt = -1;
+    int br = -1;
+    int64_t bgap = 0, bown = -8;
+    for (int64_t t = 0; t < T; ++t) {
+      const int d = o[t];
+      if (w[d] >= 0 || n[d] <= 1) continue;
+      int64_t nb[4];
+      const int k = nbrs(t, nb);
+      for (int j = 0; j < k; ++j) {
+        const int r = o[nb[j]];
+        if (r == d || w[r] <= 0 || !(P[r] + tp[r] < P[d])) continue;
+        int64_t own = 0;  // receiver-owned minus donor-owned neighbours: keep regions compact
+        for (int q = 0; q < k; ++q) own += (o[nb[q]] == r) - (o[nb[q]] == d);
+        const int64_t gap = w[r] - w[d];
+        if (bt < 0 || gap > bgap || (gap == bgap && own > bown)) {
+          bt = t;
+          br = r;
+          bgap = gap;
+          bown = own;
+        }
+      }
+    }
+    if (bt < 0) {
+      // no donor borders a receiver: the pair with the largest quota gap,
+      // donor tile nearest (Manhattan) the receiver's tiles
+      int bd = -1;
+      for (int d = 0; d < nranks; ++d)
+        if (w[d] < 0 && n[d] > 1 && (bd < 0 || w[d] < w[bd])) bd = d;
+      for (int r = 0; r < nranks; ++r)
+        if (w[r] > 0 && (br < 0 || w[r] > w[br])) br = r;
+      if (bd < 0 || br < 0 || !(P[br] + tp[br] < P[bd])) break;
+      int64_t bdist = -1;
+      for (int64_t t = 0; t < T; ++t) {
+        if (o[t] != bd) continue;
+        int64_t dist = n[br] ? -1 : 0;
+        for (int64_t u = 0; u < T && n[br]; ++u) {
+          if (o[u] != br) continue;
+          const int64_t dd = std::llabs(t % tiles_x - u % tiles_x) + std::llabs(t / tiles_x - u / tiles_x);
+          if (dist < 0 || dd < dist) dist = dd;
+        }
+        if (bdist < 0 || dist < bdist) {
+          bdist = dist;
+          bt = t;
+        }
+      }
+      if (bt < 0) break;
+    }
+    const int d = o[bt];
+    P[d] -= tp[d];
+    P[br] += tp[br];
+    o[bt] = br;
+    ++w[d];
+    --w[br];
+    --n[d];
+    ++n[br];
+    ++moved;
+  }
+  return moved;
 }
 
 }  // namespace nlh

@@ -55,4 +55,23 @@ bool resolve_owner(int64_t tiles_x, int64_t tiles_y, int32_t nranks,
 Plan make_plan(int64_t nx, int64_t ny, int64_t eps, int64_t tiles_x,
                int64_t tiles_y, const std::vector<int32_t> &owner, bool merge = true);
 
+// Load-balance policy (replaces load_balance's work_realloc and DFS/BFS tile
+// migration, src/2d_nonlocal_distributed.cpp:844-959).  busy[r] is rank r's
+// measured busy time over one window (any unit, same for all ranks).  Each
+// rank's tile quota comes from the reference's rule (:905-927): with
+// d = mean - busy[r] and the rank's own time per tile tpt = busy[r]/tiles[r],
+// quota = ceil(d/tpt) when d > 0.3 tpt, floor(d/tpt) when -d > 0.3 tpt, else 0.
+// Tiles then move one at a time from ranks with a negative quota (never their
+// last tile) to ranks with a positive one: a donor tile 4-adjacent to the
+// receiver's region first (largest quota gap, then receiver-owned minus
+// donor-owned neighbours, then lowest tile index), else the donor tile nearest the
+// receiver's region.  A move is made only if it lowers the larger of the two
+// ranks' predicted times (busy +- their own time per tile): the reference's
+// quota alone hands a tile back and forth when the tiles do not divide evenly.
+// Deterministic: every rank computes the same map.
+// Returns the number of tiles moved; owner_out holds the new map.
+int balance_owner(int64_t tiles_x, int64_t tiles_y, int32_t nranks,
+                  const std::vector<int32_t> &owner, const double *busy,
+                  std::vector<int32_t> &owner_out);
+
 }  // namespace nlh

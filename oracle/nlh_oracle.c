@@ -271,7 +271,7 @@ double nlh_oracle_run_tiled(const nlh_oracle_params *p, long nt, long tiles_x,
 /* ------------------------------------------------------------------------- */
 /* 1D solver (src/1d_nonlocal_serial.cpp)                                      */
 double nlh_oracle_c1d(long eps, double k, double dx) {
-  const long c = (long)((k * 3) / (pow(eps * dx, 3))); /* `long c_1d` (:49,57) */
+  const long c = (long)((k * 3) / (pow(eps * dx, 3))); /* `long c_1d` (1d :57,74) */
   return (double)c;
 }
 

@@ -78,7 +78,7 @@ double nlh_oracle_run_tiled(const nlh_oracle_params *p, long nt, long tiles_x,
                             long tiles_y, double *u, int nthreads);
 
 /* ---- 1D solver (src/1d_nonlocal_serial.cpp) --------------------------------
- * c_1d is declared `long` in the reference (:49,57): (k*3)/pow(eps*dx,3) is
+ * c_1d is declared `long` in the reference (1d :57,74): (k*3)/pow(eps*dx,3) is
  * truncated toward zero.  sum_local (:226-234): res += ((1.0*c_1d)*(u_j -
  * u_i))*dx over sx = x-eps .. x+eps, 0 outside [0,nx); sum_local_test
  * (:214-223): res = -(((2pi)*sin(2pi(t dt)))*sin(2pi(x dx))), res -=

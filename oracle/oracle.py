@@ -132,7 +132,7 @@ def run_tiled(p: Params, nt: int, tiles_x: int, tiles_y: int, u: np.ndarray, nth
 
 # ---- 1D solver (src/1d_nonlocal_serial.cpp) ---------------------------------
 def test_init_1d(nx: int, dx: float) -> np.ndarray:
-    """test_init(): sin(2*pi*(sx*dx)) (1d :127-132)."""
+    """test_init(): sin(2*pi*(sx*dx)) (1d :124-129)."""
     return np.array([math.sin(2 * math.pi * (sx * dx)) for sx in range(nx)], dtype=np.float64)  # libm sin
 
 

@@ -1,0 +1,152 @@
+"""GPU: dynamic load balancing (nlh_repartition / nlh_rebalance; the
+reference's load_balance, src/2d_nonlocal_distributed.cpp:844-959,
+1306-1309) on one MI355X.
+
+NLH_VIRTUAL_RANKS=V runs V owners' blocks on this GPU with the inter-owner
+pieces over RCCL (to self), so a repartition exercises the multi-rank tile
+move logic (RCCL refuses two real ranks on one device).  The field must be
+carried across the repartition untouched: the run continues bit for bit as
+the oracle (exact kernel) or within 1e-12 of field scale (fast kernels).
+"""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, read_input
+
+import nonlocalheatequation_amd as N
+
+pytestmark = pytest.mark.gpu
+
+
+def _map(name):
+    tok = read_input(name).split()
+    npx, npy = int(tok[2]), int(tok[3])
+    own = np.zeros(npx * npy, np.int32)
+    vals = list(map(int, tok[5:]))
+    for i in range(npx * npy):
+        px, py, loc = vals[3 * i:3 * i + 3]
+        own[px + py * npx] = loc
+    return npx, npy, own, int(own.max()) + 1
+
+
+def _check(oracle, u, p, t, kernel):
+    ref = oracle.run(p, t)
+    if kernel == "exact":
+        assert np.array_equal(u, ref)
+    else:
+        assert np.max(np.abs(u - ref)) <= 1e-12 * np.max(np.abs(ref))
+
+
+@pytest.mark.parametrize("kernel,test,n1,n2", [("exact", True, 4, 3), ("fast", True, 3, 4),
+                                               ("auto", False, 5, 6)])
+def test_rebalance_virtual_ranks(oracle, monkeypatch, kernel, test, n1, n2):
+    monkeypatch.setenv("NLH_VIRTUAL_RANKS", "4")
+    npx, npy, own, R = _map("load_balance_25s_4n.txt")
+    nx = ny = 5 * 48
+    eps = 6
+    dh = 1.0 / nx
+    dt = eps ** 4 * dh * dh / (8 * N.disk_count(eps))
+    p = oracle.params(nx, ny, eps, 1.0, dt, dh, int(test))
+    with N.Solver(nx, ny, eps, 1.0, dt, dh, test=test, kernel=kernel, tiles=(npx, npy), owner=own,
+                  split_tiles=False) as s:
+        s.test_init()
+        s.kernel_timing(2)
+        s.run(n1)
+        s.synchronize()
+        moved, new, busy = s.rebalance()
+        assert moved > 0 and busy.shape == (R,) and (busy > 0).all()
+        cnt = np.bincount(new, minlength=R)
+        assert cnt.max() - cnt.min() <= 1
+        assert s.step_index == n1
+        _check(oracle, s.field(), p, n1, kernel)
+        s.run(n2)
+        s.synchronize()
+        _check(oracle, s.field(), p, n1 + n2, kernel)
+        if test:
+            l2, li = s.errors(n1 + n2)
+            ref = oracle.run(p, n1 + n2)
+            rl2, rli = oracle.errors(p, n1 + n2, ref)
+            assert l2 == pytest.approx(rl2, rel=1e-9) and li == pytest.approx(rli, rel=1e-9)
+        # a second round on the balanced map moves nothing
+        assert s.rebalance()[0] == 0
+
+
+def test_repartition_explicit_maps(oracle, monkeypatch):
+    monkeypatch.setenv("NLH_VIRTUAL_RANKS", "3")
+    nx, ny, eps, tiles = 180, 120, 5, (6, 4)
+    dh = 1.0 / nx
+    dt = eps ** 4 * dh * dh / (8 * N.disk_count(eps))
+    rng = np.random.default_rng(3)
+    u0 = rng.uniform(-1, 1, size=(ny, nx))
+    p = oracle.params(nx, ny, eps, 1.0, dt, dh, 0)
+    maps = [rng.integers(0, 3, 24).astype(np.int32) for _ in range(3)]
+    with N.Solver(nx, ny, eps, 1.0, dt, dh, kernel="exact", tiles=tiles, owner=maps[0]) as s:
+        s.input_init(u0)
+        t = 0
+        for m, n in zip(maps[1:] + [maps[1]], (2, 3, 1)):
+            s.run(n)
+            t += n
+            s.repartition(m)
+            assert s.step_index == t
+        s.run(2)
+        s.synchronize()
+        ref = oracle.run(p, t + 2, u0)
+        assert np.array_equal(s.field(), ref)
+        with pytest.raises(N.NLHError):
+            s.repartition(np.full(24, 3, np.int32))  # owner outside [0, 3)
+
+
+def test_rebalance_one_rank_measured():
+    nx = ny = 256
+    eps = 4
+    dh = 1.0 / nx
+    dt = eps ** 4 * dh * dh / (8 * N.disk_count(eps))
+    with N.Solver(nx, ny, eps, 1.0, dt, dh, tiles=(2, 2)) as s:
+        s.test_init()
+        with pytest.raises(N.NLHError):
+            s.rebalance()  # busy timing is off
+        s.kernel_timing(2)
+        s.run(6)
+        ms, steps = s.kernel_time()
+        assert ms > 0 and steps == 6
+        moved, own, busy = s.rebalance()
+        assert moved == 0 and list(own) == [0, 0, 0, 0] and busy[0] == pytest.approx(ms)
+
+
+def _scaled_map(tmp_path, name, tile):
+    npx, npy, own, R = _map(name)
+    lines = [f"{tile} {tile} {npx} {npy} {1.0 / (tile * npx)}"]
+    lines += [f"{px} {py} {own[px + py * npx]}" for px in range(npx) for py in range(npy)]
+    f = tmp_path / "map.txt"
+    f.write_text("\n".join(lines) + "\n")
+    return f, npx, npy, own, R
+
+
+def test_driver_nbalance_virtual_ranks(oracle, tmp_path):
+    f, npx, npy, own, R = _scaled_map(tmp_path, "load_balance_25s_4n.txt", 32)
+    env = dict(os.environ, NLH_VIRTUAL_RANKS=str(R))
+    nt, dt = 45, 3e-5  # stable for eps 5 at dh = 1/160
+    out = subprocess.run([os.path.join(ROOT, "bin", "2d_nonlocal_distributed"), "--file", str(f),
+                          "--nt", str(nt), "--dt", str(dt), "--eps", "5", "--nbalance", "10",
+                          "--test_load_balance", "--nlog", "1000"],
+                         capture_output=True, text=True, timeout=300, env=env)
+    assert out.returncode == 0, out.stderr
+    lines = out.stdout.splitlines()
+    i = lines.index("Testing load balance:")
+    assert sum(l.startswith("Test: counter value: ") for l in lines) == R
+    assert any(l.startswith("Expected busy rate ") for l in lines)
+    j = lines.index("Visualizing Load Balance across nodes")
+    grid = [list(map(int, lines[j + 1 + r].split())) for r in range(npx)]
+    cnt = np.bincount(np.array(grid).ravel(), minlength=R)
+    assert cnt.max() - cnt.min() <= 1 and i < j
+    assert lines[j + 1 + npx] in ("Load balanced correctly", "Load not balanced correctly")
+    # the field went through 4 repartitions untouched: l2 as the oracle's
+    n = 32 * npx
+    p = oracle.params(n, n, 5, 1.0, dt, 1.0 / n, 1)
+    l2, li = oracle.errors(p, nt, oracle.run(p, nt))
+    m = re.search(r"^l2: (\S+) linfinity: (\S+)$", out.stdout, re.M)
+    assert m and float(m.group(1)) == pytest.approx(l2, rel=1e-5) and float(m.group(2)) == pytest.approx(li, rel=1e-5)

@@ -175,7 +175,7 @@ def test_oracle_1d_batch_contract(oracle):
 
 def test_oracle_1d_restatement_small(oracle):
     """The C restatement against a direct pure-Python transcription of
-    sum_local / sum_local_test / do_work (1d :186-224) on a small case."""
+    sum_local / sum_local_test / do_work (1d :186-236) on a small case."""
     import math
     nx, nt, eps, k, dt, dx = 13, 7, 3, 1.0, 0.001, 0.02
     c = float(int((k * 3) / (pow(eps * dx, 3))))
