@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define NLH_ABI_VERSION 5
+#define NLH_ABI_VERSION 6
 
 enum nlh_status {
   NLH_OK = 0,
@@ -157,6 +157,9 @@ typedef struct nlh_info {
                               pass over HBM (one halo exchange per pass)   */
   char    pass_kernel[32]; /* device kernel of one full pass: "k_pair_split",
                               "k_pair_mw", "k_pair", "k_fast" or "k_exact"  */
+  int32_t owners;          /* owner ids in the tile map: nranks, or the
+                              NLH_VIRTUAL_RANKS count (nlh_rebalance sizes) */
+  int32_t reserved_;
 } nlh_info;
 int nlh_get_info(const nlh_solver *s, nlh_info *info);
 

@@ -69,7 +69,7 @@ class _Info(ctypes.Structure):
         ("npeers", ctypes.c_int32), ("owned_nodes", ctypes.c_int64), ("disk_points", ctypes.c_int64),
         ("halo_bytes_sent", ctypes.c_int64), ("device_bytes", ctypes.c_int64),
         ("arch", ctypes.c_char * 32), ("halo_width", ctypes.c_int32), ("steps_per_pass", ctypes.c_int32),
-        ("pass_kernel", ctypes.c_char * 32),
+        ("pass_kernel", ctypes.c_char * 32), ("owners", ctypes.c_int32), ("reserved_", ctypes.c_int32),
     ]
 
 
@@ -271,6 +271,7 @@ class Info:
     halo_width: int = 0
     steps_per_pass: int = 1
     pass_kernel: str = ""
+    owners: int = 1
 
 
 class Solver:
@@ -400,7 +401,7 @@ class Solver:
         _check(lib().nlh_get_info(self._h, ctypes.byref(i)), "nlh_get_info")
         return Info(i.kernel, i.device, i.nblocks, i.npeers, i.owned_nodes, i.disk_points,
                     i.halo_bytes_sent, i.device_bytes, i.arch.decode(), i.halo_width, i.steps_per_pass,
-                    i.pass_kernel.decode())
+                    i.pass_kernel.decode(), i.owners)
 
     def kernel_timing(self, enable) -> None:
         """False/0 off; True/1 one event pair per run(); 2 busy time (every
@@ -413,12 +414,14 @@ class Solver:
         o = np.ascontiguousarray(owner, dtype=np.int32).reshape(-1)
         _check(lib().nlh_repartition(self._h, o.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))), "nlh_repartition")
 
-    def rebalance(self, busy=None, apply=True, nowners=None):
+    def rebalance(self, busy=None, apply=True):
         """Collective load-balancing round (load_balance, :1306-1309): busy
         times measured with kernel_timing(2) (or ``busy``, one per owner), the
         policy's map applied.  Returns (tiles moved, owner map, busy used)."""
         ntiles = self._tiles[0] * self._tiles[1]
-        nown = int(nowners or (len(busy) if busy is not None else self._nranks))
+        nown = self.info().owners
+        if busy is not None and len(busy) != nown:
+            raise ValueError(f"busy needs one entry per owner ({nown})")
         out = np.zeros(ntiles, dtype=np.int32)
         bo = np.zeros(nown, dtype=np.float64)
         bi = None

@@ -1388,6 +1388,7 @@ int nlh_get_info(const nlh_solver *s, nlh_info *info) {
   info->device_bytes = s->device_bytes;
   info->halo_width = s->halo;
   info->steps_per_pass = s->pair ? 2 : 1;
+  info->owners = s->owners;
   const char *pk = s->pair ? (s->pair_split == 3 ? "k_pair_pf" : s->pair_split == 2 ? "k_pair_mw"
                               : s->pair_split == 1 ? "k_pair_split" : "k_pair")
                            : s->wide ? "k_wide" : s->weighted ? "k_weighted"

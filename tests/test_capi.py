@@ -37,7 +37,7 @@ def test_python_binding_covers_header():
 
 
 def test_abi_version():
-    assert N.lib().nlh_abi_version() == 5
+    assert N.lib().nlh_abi_version() == 6
 
 
 def test_params_layout_matches_header():
