@@ -103,6 +103,13 @@ int resolve_config(const nlh_params &p, Resolved &r) {
   // parity)
   if (kern == NLH_KERNEL_AUTO) kern = NLH_KERNEL_FAST;
   if (kern == NLH_KERNEL_FAST && !nlh::fast_supported(E)) {
+    // beyond the nested-window horizons: the LDS-tile kernel with J = 1
+    if (nlh::weighted_supported(E)) {
+      r.kernel = kern;
+      r.weighted = true;
+      r.halo = E;
+      return NLH_OK;
+    }
     if (p.kernel == NLH_KERNEL_FAST)
       return fail(NLH_ERR_UNSUPPORTED, "fast kernel not instantiated for eps=" + std::to_string(E));
     kern = NLH_KERNEL_EXACT;
@@ -841,10 +848,14 @@ int create_impl(const nlh_params *pin, nlh_solver *s, ncclComm_t reuse_comm = nu
   s->sc.c2d = p.influence == NLH_INFLUENCE_LINEAR ? (p.k * 40) / pow(p.eps * p.dh, 4)
                                                   : (p.k * 8) / pow(p.eps * p.dh, 4);
   s->sc.influence = p.influence;
-  if (p.influence != NLH_INFLUENCE_CONSTANT) {
+  if (p.influence != NLH_INFLUENCE_CONSTANT || rv.weighted) {
     // J(distance/eps), distance = sqrt(dx^2+dy^2) as the reference's
-    // distance() (:224-227); wt in the reference's loop order
-    auto J = [&](long dx, long dy) { return 1.0 - sqrt((double)(dx * dx + dy * dy)) / (double)p.eps; };
+    // distance() (:224-227); wt in the reference's loop order.  J = 1 tables
+    // for k_weighted at eps 33..50
+    const bool lin = p.influence == NLH_INFLUENCE_LINEAR;
+    auto J = [&](long dx, long dy) {
+      return lin ? 1.0 - sqrt((double)(dx * dx + dy * dy)) / (double)p.eps : 1.0;
+    };
     std::vector<double> wt, qj((size_t)(E + 1) * (E + 1), 0.0);
     double jsum = 0.0;
     for (long dx = -E; dx <= E; ++dx) {

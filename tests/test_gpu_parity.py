@@ -138,7 +138,39 @@ def test_eps32_golden(kernel, test):
         assert np.max(np.abs(u - g)) <= 1e-12 * np.max(np.abs(g))
 
 
-@pytest.mark.parametrize("eps", [33, 40])
+def _disk_bound(eps, nt, dh, dt, k, c_factor, scale, test):
+    """Recursive-summation rounding bound of the per-node disk sum."""
+    E = eps
+    S = (k * c_factor) / (E * dh) ** 4 * dh * dh * dt * N.disk_count(E)
+    return nt * N.disk_count(E) * 2.0 ** -53 * S * 2 * (scale + (1.0 if test else 0.0))
+
+
+@pytest.mark.parametrize("eps", [33, 40, 50])
+@pytest.mark.parametrize("test", [False, True])
+def test_large_eps_weighted_j1(oracle, eps, test):
+    """eps 33..50 (beyond the nested-window kernels): AUTO/FAST run k_weighted
+    with J = 1 over an LDS tile; per node within 1e-12 of field scale or the
+    disk sum's rounding bound, L2 as the oracle's; EXACT stays bitwise."""
+    nx, ny, nt = 150, 133, 3
+    dh = 1.0 / nx
+    r = N.BatchRow(nx, ny, nt, eps, 1.0, 0.5 * eps ** 4 * dh * dh / (8 * N.disk_count(eps)), dh)
+    u0 = None if test else np.random.default_rng(eps).uniform(-1, 1, size=(ny, nx))
+    p = oracle.params(nx, ny, eps, r.k, r.dt, dh, int(test))
+    ref = oracle.run(p, nt, u0)
+    u, (l2, _), info = _gpu_run_j(r, test, "auto", "constant", u0)
+    assert info.pass_kernel == "k_weighted" and info.kernel == N.KERNEL_FAST
+    d = np.max(np.abs(u - ref))
+    scale = np.max(np.abs(ref))
+    assert d <= max(1e-12 * scale, _disk_bound(eps, nt, dh, r.dt, r.k, 8, scale, test)), d
+    if test:
+        l2_ref = oracle.errors(p, nt, ref)[0]
+        n = nx * ny
+        assert abs(l2 - l2_ref) <= 1e-10 * l2_ref + d * (2 * np.sqrt(n * l2_ref) + n * d)
+    ue, _, info = _gpu_run_j(r, test, "exact", "constant", u0)
+    assert info.kernel == N.KERNEL_EXACT and np.array_equal(ue, ref)
+
+
+@pytest.mark.parametrize("eps", [51, 64])
 def test_unsupported_fast_eps_falls_back_to_exact(oracle, eps):
     r = N.BatchRow(60, 50, 2, eps, 1.0, 1e-4, 1.0 / 60)
     with N.Solver(r.nx, r.ny, eps, r.k, r.dt, r.dh, test=False, kernel="auto") as s:
@@ -375,7 +407,10 @@ def test_linear_influence_multiblock_rccl_self(oracle, monkeypatch):
 
 
 def test_linear_influence_large_eps_uses_exact():
-    with N.Solver(100, 90, 40, 1.0, 1e-9, 0.01, influence="linear") as s:
+    # the LDS tile of k_weighted holds eps <= 50
+    with N.Solver(120, 110, 51, 1.0, 1e-9, 0.01, influence="linear") as s:
         assert s.info().kernel == N.KERNEL_EXACT
     with pytest.raises(N.NLHError):
-        N.Solver(100, 90, 40, 1.0, 1e-9, 0.01, influence="linear", kernel="fast")
+        N.Solver(120, 110, 51, 1.0, 1e-9, 0.01, influence="linear", kernel="fast")
+    with N.Solver(100, 90, 40, 1.0, 1e-9, 0.01, influence="linear") as s:
+        assert s.info().pass_kernel == "k_weighted"
