@@ -396,7 +396,7 @@ int build_rectlists(nlh_solver *s, int kind) {
         R.nstrip = (int)ceil_div(R.x1 - R.x0, sw);
         R.nseg = (int)ceil_div(R.y1 - R.y0, R.seg_rows);
       } else {
-        R.seg_rows = s->weighted ? 16 : 4;
+        R.seg_rows = (s->weighted || nlh::exact_lds_ok(E, s->p.test != 0)) ? 16 : 4;
         R.nstrip = (int)ceil_div(R.x1 - R.x0, 64);
         R.nseg = (int)ceil_div(R.y1 - R.y0, R.seg_rows);
       }

@@ -112,6 +112,9 @@ int launch_exact(const RectList &rl, const StepConst &c, bool test, void *stream
 // 64 x 16 outputs per workgroup, direct weighted sum over the disk's 4-fold
 // symmetric groups; rect lists as k_exact with 16-row segments
 bool weighted_supported(int E);
+// k_exact_lds (LDS-staged bit-parity kernel, 16-row segments) handles (E, test);
+// otherwise k_exact (4-row segments)
+bool exact_lds_ok(int E, bool test);
 int launch_weighted(const RectList &rl, const StepConst &c, bool test, void *stream);
 // A = sum_local(u) only (no time update) -- used once for L_h[W0].
 int launch_exact_sum(const RectList &rl, const StepConst &c, void *stream);

@@ -105,6 +105,109 @@ __global__ __launch_bounds__(256) void k_exact(RectList L, StepConst C) {
 }
 
 // ----------------------------------------------------------------------------
+// k_exact_lds: the bit-parity kernel with the lattice staged in LDS.  A
+// 256-thread workgroup owns 64 x 16 nodes; its (64+2E) x (16+2E) tile of u
+// (and in test mode of w = (ct*sin x)*sin y, 0 outside the domain: the value
+// k_exact forms per term, formed once here) sits in LDS.  Each thread runs 4
+// vertically adjacent nodes of one column through the reference's loop
+// (sx outer, sy inner; ((J*c)*(u_j-u_i))*dh^2 accumulated in order, no FMA
+// contraction), so for every (dx, dy) the 4 nodes read 4 consecutive tile
+// rows: a 4-value register window slides down the column, one LDS read per
+// term per 4 nodes.  Bitwise equal to k_exact.
+template <bool TEST, bool WT>
+__global__ __launch_bounds__(256) void k_exact_lds(RectList L, StepConst C) {
+#pragma clang fp contract(off)
+  extern __shared__ double tile[];
+  const int work = xcd_remap(blockIdx.x, gridDim.x);
+  const int ri = find_rect(L, work);
+  const Rect &R = L.r[ri];
+  const int local = work - R.wg_begin;
+  const int tx = local % R.nstrip, ty = local / R.nstrip;
+  const int E = C.E;
+  const int x0 = R.x0 + tx * 64, y0 = R.y0 + ty * 16;
+  const int TW = 64 + 2 * E, TH = 16 + 2 * E;
+  const int64_t p = R.pitch;
+  const int ylast = R.y1 + E - 1;  // rows past it only feed nodes that are not stored
+  double *wtile = tile + TW * TH;
+  for (int e = (int)threadIdx.x; e < TW * TH; e += 256) {
+    const int r = e / TW, cc = e - r * TW;
+    const int gy = min(y0 - E + r, ylast);
+    tile[e] = R.u[(int64_t)gy * p + (x0 - E + cc)];
+    if (TEST) {
+      const int sx = R.gx0 + x0 - E + cc, sy = R.gy0 + y0 - E + r;
+      const bool in = sx >= 0 && sx < C.nx && sy >= 0 && sy < C.ny;
+      wtile[e] = in ? (C.ct * C.sxt[sx + E]) * C.syt[sy + E] : 0.0;
+    }
+  }
+  __syncthreads();
+  const int lx = (int)(threadIdx.x & 63), ly = (int)(threadIdx.x >> 6) * 4;
+  const int x = x0 + lx;
+  const double *c = tile + (ly + E) * TW + (lx + E);  // node (x, y0 + ly)
+  double ui[4], res[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) ui[k] = c[k * TW];
+  const double c2d = C.c2d, dh2 = C.dh2;
+  int n = 0;
+  for (int dx = -E; dx <= E; ++dx) {
+    const int len = C.lens[dx < 0 ? -dx : dx];
+    const double *col = c + dx;
+    double v0 = col[-len * TW], v1 = col[(1 - len) * TW], v2 = col[(2 - len) * TW];
+    for (int dy = -len; dy <= len; ++dy, ++n) {
+      const double v3 = col[(dy + 3) * TW];
+      const double wv = WT ? C.wt[n] : c2d;
+      res[0] += ((wv * (v0 - ui[0])) * dh2);
+      res[1] += ((wv * (v1 - ui[1])) * dh2);
+      res[2] += ((wv * (v2 - ui[2])) * dh2);
+      res[3] += ((wv * (v3 - ui[3])) * dh2);
+      v0 = v1;
+      v1 = v2;
+      v2 = v3;
+    }
+  }
+  double r2[4], wpos[4];
+  if (TEST) {
+    const int gx = min(R.gx0 + x, C.nx - 1);  // columns past the lattice: not stored
+    const double sxv = C.sxt[gx + E];
+    const double *cw = wtile + (ly + E) * TW + (lx + E);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      // rows past the lattice only feed nodes that are not stored: clamp the
+      // table index, keep the arithmetic
+      const int gy = min(R.gy0 + y0 + ly + k, C.ny - 1);
+      const double syv = C.syt[gy + E];
+      r2[k] = -((C.st2pi * sxv) * syv);
+      wpos[k] = (C.ct * sxv) * syv;
+    }
+    n = 0;
+    for (int dx = -E; dx <= E; ++dx) {
+      const int len = C.lens[dx < 0 ? -dx : dx];
+      const double *col = cw + dx;
+      double v0 = col[-len * TW], v1 = col[(1 - len) * TW], v2 = col[(2 - len) * TW];
+      for (int dy = -len; dy <= len; ++dy, ++n) {
+        const double v3 = col[(dy + 3) * TW];
+        const double wv = WT ? C.wt[n] : c2d;
+        r2[0] -= ((wv * (v0 - wpos[0])) * dh2);
+        r2[1] -= ((wv * (v1 - wpos[1])) * dh2);
+        r2[2] -= ((wv * (v2 - wpos[2])) * dh2);
+        r2[3] -= ((wv * (v3 - wpos[3])) * dh2);
+        v0 = v1;
+        v1 = v2;
+        v2 = v3;
+      }
+    }
+  }
+  if (x >= R.x1) return;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int y = y0 + ly + k;
+    if (y >= R.y1) break;
+    double out = ui[k] + (res[k] * C.dt);
+    if (TEST) out += r2[k] * C.dt;
+    R.un[(int64_t)y * p + x] = out;
+  }
+}
+
+// ----------------------------------------------------------------------------
 // k_weighted: fast path for a non-constant radial J (influence != 0), and for
 // J = 1 beyond the nested-window kernels' horizons (eps 33..50).  The
 // nested-window kernels need J = 1; here each 256-thread workgroup stages a
@@ -470,9 +573,26 @@ int launch_fast(const RectList &rl, const StepConst &c, bool test, int want_r, v
   return -1;
 }
 
+// k_exact_lds's tile(s) at two workgroups per CU at least
+bool exact_lds_ok(int E, bool test) {
+  return (size_t)(64 + 2 * E) * (16 + 2 * E) * sizeof(double) * (test ? 2 : 1) <= 80 * 1024;
+}
+
 int launch_exact(const RectList &rl, const StepConst &c, bool test, void *stream) {
   hipStream_t st = (hipStream_t)stream;
   const bool wt = c.influence != 0;
+  if (exact_lds_ok(c.E, test)) {  // rects built with 16-row segments (build_rectlists)
+    const size_t shm = (size_t)(64 + 2 * c.E) * (16 + 2 * c.E) * sizeof(double) * (test ? 2 : 1);
+    if (test && wt)
+      hipLaunchKernelGGL((k_exact_lds<true, true>), dim3(rl.nwork), dim3(256), shm, st, rl, c);
+    else if (test)
+      hipLaunchKernelGGL((k_exact_lds<true, false>), dim3(rl.nwork), dim3(256), shm, st, rl, c);
+    else if (wt)
+      hipLaunchKernelGGL((k_exact_lds<false, true>), dim3(rl.nwork), dim3(256), shm, st, rl, c);
+    else
+      hipLaunchKernelGGL((k_exact_lds<false, false>), dim3(rl.nwork), dim3(256), shm, st, rl, c);
+    return check_launch();
+  }
   if (test && wt)
     hipLaunchKernelGGL((k_exact<true, false, true>), dim3(rl.nwork), dim3(256), 0, st, rl, c);
   else if (test)
