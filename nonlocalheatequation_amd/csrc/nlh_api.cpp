@@ -851,7 +851,7 @@ int create_impl(const nlh_params *pin, nlh_solver *s, ncclComm_t reuse_comm = nu
   if (p.influence != NLH_INFLUENCE_CONSTANT || rv.weighted) {
     // J(distance/eps), distance = sqrt(dx^2+dy^2) as the reference's
     // distance() (:224-227); wt in the reference's loop order.  J = 1 tables
-    // for k_weighted at eps 33..50
+    // for k_weighted at eps 33..52
     const bool lin = p.influence == NLH_INFLUENCE_LINEAR;
     auto J = [&](long dx, long dy) {
       return lin ? 1.0 - sqrt((double)(dx * dx + dy * dy)) / (double)p.eps : 1.0;

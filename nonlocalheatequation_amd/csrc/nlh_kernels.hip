@@ -209,7 +209,7 @@ __global__ __launch_bounds__(256) void k_exact_lds(RectList L, StepConst C) {
 
 // ----------------------------------------------------------------------------
 // k_weighted: fast path for a non-constant radial J (influence != 0), and for
-// J = 1 beyond the nested-window kernels' horizons (eps 33..50).  The
+// J = 1 beyond the nested-window kernels' horizons (eps 33..52).  The
 // nested-window kernels need J = 1; here each 256-thread workgroup stages a
 // (64+2E) x (16+2E) tile of u in LDS (rows past the block clamp to its last
 // halo row; they only feed outputs that are not stored) and each thread
@@ -614,7 +614,7 @@ int launch_exact_sum(const RectList &rl, const StepConst &c, void *stream) {
   return check_launch();
 }
 
-// the (64+2E) x (16+2E) fp64 tile within the 160 KB LDS of a CU: E <= 50
+// the (64+2E) x (16+2E) fp64 tile within the 160 KB LDS of a CU: E <= 52
 bool weighted_supported(int E) {
   return E >= 1 && (size_t)(64 + 2 * E) * (16 + 2 * E) * sizeof(double) <= 160 * 1024;
 }
