@@ -83,8 +83,18 @@ def test_single_rank_owner_map_from_file(oracle):
     assert np.array_equal(u, oracle.run(p, 10))
 
 
-def _rccl_rank(rank, cid, ndev, q):
+def _rccl_rank(rank, idq, q):
     try:
+        import torch
+        ndev = max(1, torch.cuda.device_count())  # counting only: no GPU init
+        # rank 0 makes the RCCL unique id and hands it to rank 1; the parent
+        # process never touches RCCL (an unused id's bootstrap root thread
+        # would outlive the test in it)
+        if rank == 0:
+            cid = N.comm_unique_id()
+            idq.put(cid)
+        else:
+            cid = idq.get(timeout=120)
         nx = ny = 256
         eps = 8
         dh = 1.0 / nx
@@ -96,9 +106,9 @@ def _rccl_rank(rank, cid, ndev, q):
             s.synchronize()
             u = s.gather(0)
             l2, li = s.errors(5)
-            q.put((rank, "ok", (u if rank == 0 else None, li)))
+            q.put((rank, "ok", (u if rank == 0 else None, li), ndev))
     except Exception as e:  # noqa: BLE001
-        q.put((rank, "err", str(e)))
+        q.put((rank, "err", str(e), locals().get("ndev", 1)))
 
 
 def test_rccl_two_ranks(oracle):
@@ -107,19 +117,19 @@ def test_rccl_two_ranks(oracle):
     device 0, which RCCL refuses at communicator creation ("Duplicate GPU
     detected", ncclInvalidUsage from ncclCommInitRank) -- only that exact
     refusal is a skip; any other failure (e.g. in the grouped send/recv) fails."""
-    import torch
-    ndev = max(1, torch.cuda.device_count())
-    cid = N.comm_unique_id()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_rccl_rank, args=(r, cid, ndev, q)) for r in range(2)]
+    idq = ctx.Queue()
+    ps = [ctx.Process(target=_rccl_rank, args=(r, idq, q)) for r in range(2)]
     for p in ps:
         p.start()
     res = {}
+    ndev = 1
     try:
         for _ in range(2):
-            r, st, v = q.get(timeout=180)
+            r, st, v, nd = q.get(timeout=180)
             res[r] = (st, v)
+            ndev = nd
     finally:
         for p in ps:
             p.join(timeout=30)
