@@ -1,6 +1,7 @@
 # Build of the MI355X-native nonlocal heat-equation solver.
 #   libnlh.so   C-ABI solver library (HIP kernels for gfx950 + RCCL)
 #   bin/2d_nonlocal_{serial,async,distributed}, bin/1d_nonlocal_serial   drop-in CLI drivers
+#   bin/2d_domain_decomposition   --file partition writer (host-only)
 #   oracle/liboracle.so   CPU checker (test infrastructure only)
 ROCM    ?= /opt/rocm
 HIPCC   ?= $(ROCM)/bin/hipcc
@@ -24,7 +25,7 @@ LIB_OBJS := $(OBJDIR)/nlh_kernels.o $(FAST_OBJS) $(OBJDIR)/nlh_api.o $(OBJDIR)/n
 # size cap so every accumulator stays in registers (no scratch)
 UNROLL  := -mllvm -pragma-unroll-threshold=1000000
 DRIVERS  := $(BINDIR)/2d_nonlocal_serial $(BINDIR)/2d_nonlocal_async $(BINDIR)/2d_nonlocal_distributed \
-            $(BINDIR)/1d_nonlocal_serial
+            $(BINDIR)/1d_nonlocal_serial $(BINDIR)/2d_domain_decomposition
 DRV_COMMON := $(OBJDIR)/driver_common.o $(OBJDIR)/vtu_writer.o
 
 all: lib drivers oracle

@@ -194,6 +194,14 @@ int nlh_resolve_owner(int64_t tiles_x, int64_t tiles_y, int32_t nranks,
 int nlh_balance_owner(int64_t tiles_x, int64_t tiles_y, int32_t nranks, const int32_t *owner,
                       const double *busy, int32_t *owner_out);
 
+/* Host-only static partitioner (replaces the GMSH/METIS step of the
+ * reference's 2d_domain_decomposition tool, src/domain_decomposition.cpp:
+ * 158-187): recursive coordinate bisection of the tiles_x x tiles_y tile grid
+ * into nparts rectangles of tiles, balanced by tile_weight (tiles_x*tiles_y
+ * entries, NULL = 1 each).  owner_out as nlh_params.owner.                 */
+int nlh_partition_tiles(int64_t tiles_x, int64_t tiles_y, int32_t nparts, const double *tile_weight,
+                        int32_t *owner_out);
+
 /* Collective: move to a new tile -> rank map (tiles_x*tiles_y entries, as
  * nlh_params.owner).  Tiles whose owner changes travel over RCCL (ncclSend /
  * ncclRecv of their interiors, nothing else); blocks, halo plan and exchange

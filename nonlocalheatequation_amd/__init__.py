@@ -31,6 +31,7 @@ __all__ = [
     "KERNEL_AUTO", "KERNEL_EXACT", "KERNEL_FAST", "INFLUENCE_CONSTANT", "INFLUENCE_LINEAR", "NLHError", "Solver",
     "lib", "lib_path", "comm_unique_id", "resolve_owner", "halo_plan", "block_plan",
     "disk_count", "batch_tester", "BatchRow", "Solver1D", "batch_tester_1d", "balance_owner",
+    "partition_tiles",
 ]
 
 KERNEL_AUTO, KERNEL_EXACT, KERNEL_FAST = 0, 1, 2
@@ -112,6 +113,8 @@ _SIGNATURES = {
                        ctypes.c_int64),
     "nlh_balance_owner": ([ctypes.c_int64, ctypes.c_int64, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32),
                            ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
+    "nlh_partition_tiles": ([ctypes.c_int64, ctypes.c_int64, ctypes.c_int32, ctypes.POINTER(ctypes.c_double),
+                             ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
     "nlh_repartition": ([ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
     "nlh_rebalance": ([ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.c_int32,
                        ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
@@ -246,6 +249,22 @@ def balance_owner(tiles, nranks, owner, busy):
     if moved < 0:
         _check(-moved, "nlh_balance_owner")
     return moved, out
+
+
+def partition_tiles(tiles, nparts, weight=None) -> np.ndarray:
+    """Static partition of the tile grid (nlh_partition_tiles: recursive
+    coordinate bisection, replacing the reference's METIS step,
+    src/domain_decomposition.cpp:158-187).  Owner per tile, index gx + gy*tx."""
+    tx, ty = int(tiles[0]), int(tiles[1])
+    out = np.zeros(tx * ty, dtype=np.int32)
+    w = None
+    if weight is not None:
+        w = np.ascontiguousarray(weight, dtype=np.float64).reshape(-1)
+        if w.size != tx * ty:
+            raise ValueError("weight needs tiles_x*tiles_y entries")
+    _check(lib().nlh_partition_tiles(tx, ty, int(nparts), _dp(w) if w is not None else None,
+                                     out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))), "nlh_partition_tiles")
+    return out
 
 
 def disk_count(eps: int) -> int:

@@ -1527,6 +1527,18 @@ int nlh_balance_owner(int64_t tiles_x, int64_t tiles_y, int32_t nranks, const in
   return moved;
 }
 
+int nlh_partition_tiles(int64_t tiles_x, int64_t tiles_y, int32_t nparts, const double *tile_weight,
+                        int32_t *owner_out) {
+  if (tiles_x < 1 || tiles_y < 1 || nparts < 1 || !owner_out) return fail(NLH_ERR_ARG, "bad argument");
+  if (tile_weight)
+    for (int64_t i = 0; i < tiles_x * tiles_y; ++i)
+      if (!(tile_weight[i] >= 0.0)) return fail(NLH_ERR_ARG, "tile weights must be finite and >= 0");
+  std::vector<int32_t> o;
+  nlh::partition_tiles(tiles_x, tiles_y, nparts, tile_weight, o);
+  std::memcpy(owner_out, o.data(), o.size() * sizeof(int32_t));
+  return NLH_OK;
+}
+
 int nlh_repartition(nlh_solver *s, const int32_t *owner) {
   if (!s || !owner) return fail(NLH_ERR_ARG, "null argument");
   std::vector<int32_t> o;

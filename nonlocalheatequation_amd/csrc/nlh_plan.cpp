@@ -2,6 +2,7 @@
 #include "nlh_plan.h"
 
 #include <algorithm>
+#include <cstdint>
 #include <cmath>
 #include <cstdlib>
 
@@ -108,6 +109,98 @@ Plan make_plan(int64_t nx, int64_t ny, int64_t eps, int64_t tiles_x,
     }
   }
   return plan;
+}
+
+namespace {
+bool connected(int64_t tx, const std::vector<int64_t> &tiles) {
+  if (tiles.size() <= 1) return true;
+  std::vector<int64_t> sorted(tiles);
+  std::sort(sorted.begin(), sorted.end());
+  auto has = [&](int64_t t) { return std::binary_search(sorted.begin(), sorted.end(), t); };
+  std::vector<int64_t> stack{sorted[0]}, seen{sorted[0]};
+  while (!stack.empty()) {
+    const int64_t t = stack.back();
+    stack.pop_back();
+    const int64_t x = t % tx;
+    const int64_t nb[4] = {x > 0 ? t - 1 : -1, x + 1 < tx ? t + 1 : -1, t - tx, t + tx};
+    for (int64_t u : nb) {
+      if (u < 0 || !has(u) || std::find(seen.begin(), seen.end(), u) != seen.end()) continue;
+      seen.push_back(u);
+      stack.push_back(u);
+    }
+  }
+  return seen.size() == sorted.size();
+}
+
+// bisect a set of tiles: order it along the longer side of its bounding box
+// (the other coordinate second, so a prefix is whole lines plus part of one,
+// a staircase that stays connected) and cut where the weight divides in the
+// ratio of the parts on either side
+void rcb(int64_t tx, const double *w, std::vector<int64_t> tiles, int32_t r0, int32_t nr,
+         std::vector<int32_t> &o) {
+  if (nr <= 1 || tiles.size() <= 1) {
+    for (int64_t t : tiles) o[t] = r0;
+    return;
+  }
+  int64_t x0 = tx, x1 = -1, y0 = INT64_MAX, y1 = -1;
+  for (int64_t t : tiles) {
+    x0 = std::min(x0, t % tx);
+    x1 = std::max(x1, t % tx);
+    y0 = std::min(y0, t / tx);
+    y1 = std::max(y1, t / tx);
+  }
+  const bool cols = (x1 - x0) >= (y1 - y0);  // cut across the longer side
+  std::sort(tiles.begin(), tiles.end(), [&](int64_t a, int64_t b) {
+    const int64_t pa = cols ? a % tx : a / tx, pb = cols ? b % tx : b / tx;
+    if (pa != pb) return pa < pb;
+    return (cols ? a / tx : a % tx) < (cols ? b / tx : b % tx);
+  });
+  const int32_t nl = nr / 2;
+  double total = 0.0;
+  for (int64_t t : tiles) total += w ? w[t] : 1.0;
+  const double target = total * nl / nr;
+  size_t cut = 1;
+  double cum = w ? w[tiles[0]] : 1.0, best = std::fabs(cum - target);
+  for (size_t k = 2; k < tiles.size(); ++k) {  // first k tiles to the lower parts
+    cum += w ? w[tiles[k - 1]] : 1.0;
+    const double d = std::fabs(cum - target);
+    if (d < best) {
+      best = d;
+      cut = k;
+    }
+  }
+  std::vector<int64_t> lo(tiles.begin(), tiles.begin() + cut), hi(tiles.begin() + cut, tiles.end());
+  // the cut line is split; if taking its low end leaves either side in two
+  // pieces, take its high end instead (same count, so the same weights with
+  // unit weights)
+  if (!(connected(tx, lo) && connected(tx, hi))) {
+    auto line = [&](int64_t t) { return cols ? t % tx : t / tx; };
+    const int64_t L = line(tiles[cut]);
+    size_t b = cut, e = cut;
+    while (b > 0 && line(tiles[b - 1]) == L) --b;
+    while (e < tiles.size() && line(tiles[e]) == L) ++e;
+    if (b < cut) {  // m = cut - b tiles of line L go low: try the top m instead
+      std::vector<int64_t> lo2(tiles.begin(), tiles.begin() + b), hi2;
+      lo2.insert(lo2.end(), tiles.begin() + (e - (cut - b)), tiles.begin() + e);
+      hi2.insert(hi2.end(), tiles.begin() + b, tiles.begin() + (e - (cut - b)));
+      hi2.insert(hi2.end(), tiles.begin() + e, tiles.end());
+      if (connected(tx, lo2) && connected(tx, hi2)) {
+        lo.swap(lo2);
+        hi.swap(hi2);
+      }
+    }
+  }
+  rcb(tx, w, lo, r0, nl, o);
+  rcb(tx, w, hi, r0 + nl, nr - nl, o);
+}
+}  // namespace
+
+void partition_tiles(int64_t tiles_x, int64_t tiles_y, int32_t nparts, const double *weight,
+                     std::vector<int32_t> &owner_out) {
+  owner_out.assign((size_t)(tiles_x * tiles_y), 0);
+  std::vector<int64_t> all((size_t)(tiles_x * tiles_y));
+  for (size_t i = 0; i < all.size(); ++i) all[i] = (int64_t)i;
+  rcb(tiles_x, weight, all, 0, std::max<int32_t>(1, nparts), owner_out);
 }
 
 int balance_owner(int64_t tiles_x, int64_t tiles_y, int32_t nranks,

@@ -70,6 +70,17 @@ Plan make_plan(int64_t nx, int64_t ny, int64_t eps, int64_t tiles_x,
 // quota alone hands a tile back and forth when the tiles do not divide evenly.
 // Deterministic: every rank computes the same map.
 // Returns the number of tiles moved; owner_out holds the new map.
+// Static partitioner replacing the GMSH/METIS step of the reference's
+// 2d_domain_decomposition tool (src/domain_decomposition.cpp:158-187,
+// METIS_PartMeshDual on the coarse tile mesh): recursive coordinate bisection
+// of the tile grid -- order the current set of tiles along the longer side of
+// its bounding box and cut where the tile weight (1 each if `weight` is null)
+// divides in the ratio of the parts on either side, recurse.  Parts are
+// whole lines of tiles plus at most a partial line (connected staircases,
+// short boundaries); parts beyond the tile count stay empty.
+void partition_tiles(int64_t tiles_x, int64_t tiles_y, int32_t nparts, const double *weight,
+                     std::vector<int32_t> &owner_out);
+
 int balance_owner(int64_t tiles_x, int64_t tiles_y, int32_t nranks,
                   const std::vector<int32_t> &owner, const double *busy,
                   std::vector<int32_t> &owner_out);

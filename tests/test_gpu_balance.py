@@ -155,3 +155,22 @@ def test_driver_nbalance_virtual_ranks(oracle, tmp_path):
     l2, li = oracle.errors(p, nt, oracle.run(p, nt))
     m = re.search(r"^l2: (\S+) linfinity: (\S+)$", out.stdout, re.M)
     assert m and float(m.group(1)) == pytest.approx(l2, rel=1e-5) and float(m.group(2)) == pytest.approx(li, rel=1e-5)
+
+
+def test_driver_runs_partitioner_file(oracle, tmp_path):
+    """bin/2d_domain_decomposition (RCB partitioner) -> --file -> the
+    distributed driver over 4 virtual owners: same L2 as the oracle."""
+    f = tmp_path / "rcb.txt"
+    p = subprocess.run([os.path.join(ROOT, "bin", "2d_domain_decomposition"), "160x160:0.00625", str(f), "4"],
+                       input="32\n32\n", capture_output=True, text=True, timeout=60)
+    assert p.returncode == 0, p.stderr
+    env = dict(os.environ, NLH_VIRTUAL_RANKS="4")
+    nt, dt = 20, 3e-5
+    out = subprocess.run([os.path.join(ROOT, "bin", "2d_nonlocal_distributed"), "--file", str(f), "--nt", str(nt),
+                          "--dt", str(dt), "--eps", "5", "--nlog", "1000"],
+                         capture_output=True, text=True, timeout=300, env=env)
+    assert out.returncode == 0, out.stderr
+    pp = oracle.params(160, 160, 5, 1.0, dt, 0.00625, 1)
+    l2, li = oracle.errors(pp, nt, oracle.run(pp, nt))
+    m = re.search(r"^l2: (\S+) linfinity: (\S+)$", out.stdout, re.M)
+    assert m and float(m.group(1)) == pytest.approx(l2, rel=1e-5) and float(m.group(2)) == pytest.approx(li, rel=1e-5)
