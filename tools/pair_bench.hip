@@ -78,13 +78,17 @@ int main(int argc, char **argv) {
   CK(hipGetDeviceProperties(&prop, 0));
   const int cus = prop.multiProcessorCount;
 
-  // ablation masks of k_pair_split: 2 no HBM, 4 no LDS window reads,
-  // 8 no s_barrier, 16 no u^{t+1} LDS writes
+  // ablation masks of k_pair_split (nlh_pair.h): 4 no LDS window reads,
+  // 8 no s_barrier, 16 no u^{t+1} LDS writes, 32 no checks, 64 no vmcnt
+  // wait, 128 no store, 256 no DMA, 512 nt stores, 1024 nt DMA; 452 = VALU
+  // only (no LDS reads, no vmcnt waits, no stores, no DMA)
   std::vector<Variant> vs = {
       {"split_D8_B4", k_pair_split<E, 8, 0, 4>, 128, 4, 128 - 2 * E},
       {"split_abl512_ntstore", k_pair_split<E, 8, 512, 4>, 128, 4, 128 - 2 * E},
       {"split_abl1024_tDMA", k_pair_split<E, 8, 1024, 4>, 128, 4, 128 - 2 * E},
       {"split_abl1536_ntstore_tDMA", k_pair_split<E, 8, 1536, 4>, 128, 4, 128 - 2 * E},
+      {"abl_no_dma_no_store", k_pair_split<E, 8, 384, 4>, 128, 4, 128 - 2 * E},
+      {"abl_valu_only", k_pair_split<E, 8, 452, 4>, 128, 4, 128 - 2 * E},
       {"split_D8_B4_seg76", k_pair_split<E, 8, 0, 4>, 128, 8, 128 - 2 * E},
       {"split_D8_B4_seg304", k_pair_split<E, 8, 0, 4>, 128, 2, 128 - 2 * E},
   };
