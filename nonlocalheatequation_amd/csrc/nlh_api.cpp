@@ -1403,7 +1403,8 @@ int nlh_get_info(const nlh_solver *s, nlh_info *info) {
   const char *pk = s->pair ? (s->pair_split == 3 ? "k_pair_pf" : s->pair_split == 2 ? "k_pair_mw"
                               : s->pair_split == 1 ? "k_pair_split" : "k_pair")
                            : s->wide ? "k_wide" : s->weighted ? "k_weighted"
-                           : (s->kernel == NLH_KERNEL_FAST ? "k_fast" : "k_exact");
+                           : s->kernel == NLH_KERNEL_FAST ? "k_fast"
+                           : nlh::exact_lds_ok((int)s->p.eps, s->p.test != 0) ? "k_exact_lds" : "k_exact";
   std::snprintf(info->pass_kernel, sizeof(info->pass_kernel), "%s", pk);
   std::snprintf(info->arch, sizeof(info->arch), "%s", s->arch);
   return NLH_OK;
