@@ -40,7 +40,11 @@ __global__ __launch_bounds__(64) void k_fast(RectList L, StepConst C) {
   constexpr int KC = E + 1;             // centre-ring slots (CR)
   constexpr int GU = (NCH + 63) / 64;   // DMA instructions per u row
   constexpr int GL = TEST ? (W / 2 + 63) / 64 : 0;  // per L_h[W0] row
-  constexpr int G = GU + GL;
+  // TEST: the sin(2 pi y dh) table entry of the row too, one 16-byte DMA: a
+  // scalar load per row stalls the lone wave of a SIMD on every row (the
+  // lgkmcnt wait for the LDS window also waits for it), 64% wait cycles
+  constexpr int GS = TEST ? 1 : 0;
+  constexpr int G = GU + GL + GS;
   constexpr int OFF = EP - E;           // window start inside a staged row
   static_assert(D >= 1, "prefetch distance");
   // gfx950 counts global stores in vmcnt too: once every one of the last D
@@ -48,9 +52,10 @@ __global__ __launch_bounds__(64) void k_fast(RectList L, StepConst C) {
   // lane 0 always owns a column) the wait for row i admits D more ops
   static_assert(D * G + D < 64, "vmcnt range");
 
-  __shared__ __attribute__((aligned(16))) double ring[K * RW + (TEST ? K * W : 0) + (CR ? KC * W : 0)];
+  __shared__ __attribute__((aligned(16))) double ring[K * RW + (TEST ? K * W + 2 * K : 0) + (CR ? KC * W : 0)];
   double *lwr = ring + K * RW;                          // L_h[W0] ring (TEST)
-  double *cring = ring + K * RW + (TEST ? K * W : 0);   // centre ring (CR)
+  double *syr = lwr + K * W;                            // sin(2 pi y dh) pairs (TEST)
+  double *cring = ring + K * RW + (TEST ? K * W + 2 * K : 0);   // centre ring (CR)
 
   const int lane = (int)threadIdx.x;
   const int work = (ABL & 4) ? (int)blockIdx.x : xcd_remap(blockIdx.x, gridDim.x);
@@ -82,6 +87,12 @@ __global__ __launch_bounds__(64) void k_fast(RectList L, StepConst C) {
   const double *l0 = TEST ? Rc.lw + (int64_t)(up ? Y1 - 1 : Y0) * pitch + x0 : nullptr;
   const uint32_t lring = __builtin_amdgcn_readfirstlane(lds_addr(ring));
   const uint32_t llw = __builtin_amdgcn_readfirstlane(lds_addr(lwr));
+  const uint32_t lsy = __builtin_amdgcn_readfirstlane(lds_addr(syr));
+  // table index of sin(2 pi y dh) for the output of iteration i
+  auto sy_index = [&](int i) {
+    const int lr = min(max(i - 2 * E, 0), n_in - 2 * E - 1);
+    return rgy0 + (up ? Y1 - 1 - lr : Y0 + lr) + E;
+  };
 
   const int xl = x0 + R * lane;  // first column of this lane
   double sxv[R];
@@ -103,6 +114,7 @@ __global__ __launch_bounds__(64) void k_fast(RectList L, StepConst C) {
     if (TEST) {
       const int lr = min(max(i - 2 * E, 0), n_in - 2 * E - 1);
       dma_chunks<W / 2>(l0 + (int64_t)lr * stride, llw + slot * W * 8, lane);
+      dma_chunks<1>(C.syt + (sy_index(i) & ~1), lsy + slot * 16, lane);
     }
   };
 
@@ -187,8 +199,7 @@ __global__ __launch_bounds__(64) void k_fast(RectList L, StepConst C) {
             out[c] = fma(diff, alpha, uc);
           }
           if (TEST) {
-            const int y = up ? (Y1 - 1 - (i - 2 * E)) : (Y0 + i - 2 * E);
-            const double syv = C.syt[rgy0 + y + E];
+            const double syv = syr[2 * slot + (sy_index(i) & 1)];
             const double *lrow = lwr + slot * W + R * lane;
 #pragma unroll
             for (int c = 0; c < R; ++c) {

@@ -85,14 +85,16 @@ __global__ __launch_bounds__(64, 1) void k_wide(RectList L, StepConst C) {
   constexpr int K = pow2_ceil(D + 1);   // ring slots
   constexpr int GU = (AB ? 2 : 1) * ((NCH + 63) / 64);  // DMA instructions per u row
   constexpr int GL = TEST ? (W / 2 + 63) / 64 : 0;  // per L_h[W0] row
-  constexpr int G = GU + GL;
+  constexpr int GS = TEST ? 1 : 0;  // the row's sin(2 pi y dh) pair (no scalar load per row)
+  constexpr int G = GU + GL + GS;
   constexpr int NA = 2 * E + CH;        // live accumulators
   constexpr int NG = (E + kWideLG - 1) / kWideLG;  // level groups
   static_assert(D * G + CH < 64, "vmcnt range");
   static_assert(CH % PIN == 0, "rows per pin");
 
-  __shared__ __attribute__((aligned(16))) double ring[K * RWS + (TEST ? K * W : 0)];
+  __shared__ __attribute__((aligned(16))) double ring[K * RWS + (TEST ? K * W + 2 * K : 0)];
   double *lwr = ring + K * RWS;  // L_h[W0] rows (TEST), same slots as the u rows
+  double *syr = lwr + K * W;     // sin(2 pi y dh) pairs (TEST), same slots
 
   const int lane = (int)threadIdx.x;
   const int work = xcd_remap(blockIdx.x, gridDim.x);
@@ -127,6 +129,12 @@ __global__ __launch_bounds__(64, 1) void k_wide(RectList L, StepConst C) {
   const int lane_off = (s_l & 1) ? OB + s_l - 1 : s_l;
   const uint32_t lring = __builtin_amdgcn_readfirstlane(lds_addr(ring));
   const uint32_t llw = __builtin_amdgcn_readfirstlane(lds_addr(lwr));
+  const uint32_t lsy = __builtin_amdgcn_readfirstlane(lds_addr(syr));
+  // table index of sin(2 pi y dh) for output k = i - E of input row i
+  auto sy_index = [&](int i) {
+    const int k = min(max(i - E, 0), nout - 1);
+    return rgy0 + (up ? Y1 - 1 - k : Y0 + k) + E;
+  };
   // u rows: running pointer clamped at the last input row
   const double *gnext = ru + (int64_t)yfirst * pitch + (x0 - EP);
   // L_h[W0] row of output k = i - E (the centre row of input i), fetched with
@@ -138,6 +146,7 @@ __global__ __launch_bounds__(64, 1) void k_wide(RectList L, StepConst C) {
     if constexpr (TEST) {
       const int k = min(fetched, n_in - 1) - E;
       dma_chunks<W / 2>(l0 + (int64_t)k * stride, llw + slot * W * 8, lane);
+      dma_chunks<1>(C.syt + (sy_index(fetched) & ~1), lsy + slot * 16, lane);
     }
     dma_chunks<NCH>(gnext, lring + slot * RWS * 8, lane);
     if constexpr (AB) dma_chunks<NCH>(gnext + 1, lring + (slot * RWS + OB) * 8, lane);
@@ -293,9 +302,7 @@ __global__ __launch_bounds__(64, 1) void k_wide(RectList L, StepConst C) {
       acc[c + E] = fma(kc, wc, acc[c + E]);
       if constexpr (TEST) {
         // b = -(2 pi st) W0 - ct L_h[W0] at output k = i - E
-        const int k = i - E;
-        const int y = up ? (Y1 - 1 - k) : (Y0 + k);
-        const double syv = C.syt[rgy0 + y + E];
+        const double syv = syr[2 * (i & (K - 1)) + (sy_index(i) & 1)];
         const double b = -(C.st2pi * (sxv * syv)) - C.ct * lwr[(i & (K - 1)) * W + lane];
         acc[c + E] = fma(qs, b, acc[c + E]);
       }
