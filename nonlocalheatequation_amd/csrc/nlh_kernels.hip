@@ -147,22 +147,46 @@ __global__ __launch_bounds__(256) void k_exact_lds(RectList L, StepConst C) {
 #pragma unroll
   for (int k = 0; k < 4; ++k) ui[k] = c[k * TW];
   const double c2d = C.c2d, dh2 = C.dh2;
-  int n = 0;
-  for (int dx = -E; dx <= E; ++dx) {
-    const int len = C.lens[dx < 0 ? -dx : dx];
-    const double *col = c + dx;
+  // one disk column: 4 nodes, terms in the reference's dy order each; four dy
+  // per iteration so the window slides by renaming (3 moves per 4 dy) and the
+  // 4 LDS reads of a block are in flight together
+  auto column = [&](const double *col, int len, int n, double (&acc)[4], const double (&ref)[4],
+                    bool sub) __attribute__((always_inline)) {
     double v0 = col[-len * TW], v1 = col[(1 - len) * TW], v2 = col[(2 - len) * TW];
-    for (int dy = -len; dy <= len; ++dy, ++n) {
+    auto term = [&](double &a, double wv, double v, double r) __attribute__((always_inline)) {
+      if (sub)
+        a -= ((wv * (v - r)) * dh2);
+      else
+        a += ((wv * (v - r)) * dh2);
+    };
+    int dy = -len;
+    for (; dy + 3 <= len; dy += 4, n += 4) {
+      const double v3 = col[(dy + 3) * TW], v4 = col[(dy + 4) * TW], v5 = col[(dy + 5) * TW],
+                   v6 = col[(dy + 6) * TW];
+      const double w0 = WT ? C.wt[n] : c2d, w1 = WT ? C.wt[n + 1] : c2d, w2 = WT ? C.wt[n + 2] : c2d,
+                   w3 = WT ? C.wt[n + 3] : c2d;
+      term(acc[0], w0, v0, ref[0]); term(acc[1], w0, v1, ref[1]); term(acc[2], w0, v2, ref[2]); term(acc[3], w0, v3, ref[3]);
+      term(acc[0], w1, v1, ref[0]); term(acc[1], w1, v2, ref[1]); term(acc[2], w1, v3, ref[2]); term(acc[3], w1, v4, ref[3]);
+      term(acc[0], w2, v2, ref[0]); term(acc[1], w2, v3, ref[1]); term(acc[2], w2, v4, ref[2]); term(acc[3], w2, v5, ref[3]);
+      term(acc[0], w3, v3, ref[0]); term(acc[1], w3, v4, ref[1]); term(acc[2], w3, v5, ref[2]); term(acc[3], w3, v6, ref[3]);
+      v0 = v4;
+      v1 = v5;
+      v2 = v6;
+    }
+    for (; dy <= len; ++dy, ++n) {
       const double v3 = col[(dy + 3) * TW];
       const double wv = WT ? C.wt[n] : c2d;
-      res[0] += ((wv * (v0 - ui[0])) * dh2);
-      res[1] += ((wv * (v1 - ui[1])) * dh2);
-      res[2] += ((wv * (v2 - ui[2])) * dh2);
-      res[3] += ((wv * (v3 - ui[3])) * dh2);
+      term(acc[0], wv, v0, ref[0]); term(acc[1], wv, v1, ref[1]); term(acc[2], wv, v2, ref[2]); term(acc[3], wv, v3, ref[3]);
       v0 = v1;
       v1 = v2;
       v2 = v3;
     }
+  };
+  int n = 0;
+  for (int dx = -E; dx <= E; ++dx) {
+    const int len = C.lens[dx < 0 ? -dx : dx];
+    column(c + dx, len, n, res, ui, false);
+    n += 2 * len + 1;
   }
   double r2[4], wpos[4];
   if (TEST) {
@@ -181,19 +205,8 @@ __global__ __launch_bounds__(256) void k_exact_lds(RectList L, StepConst C) {
     n = 0;
     for (int dx = -E; dx <= E; ++dx) {
       const int len = C.lens[dx < 0 ? -dx : dx];
-      const double *col = cw + dx;
-      double v0 = col[-len * TW], v1 = col[(1 - len) * TW], v2 = col[(2 - len) * TW];
-      for (int dy = -len; dy <= len; ++dy, ++n) {
-        const double v3 = col[(dy + 3) * TW];
-        const double wv = WT ? C.wt[n] : c2d;
-        r2[0] -= ((wv * (v0 - wpos[0])) * dh2);
-        r2[1] -= ((wv * (v1 - wpos[1])) * dh2);
-        r2[2] -= ((wv * (v2 - wpos[2])) * dh2);
-        r2[3] -= ((wv * (v3 - wpos[3])) * dh2);
-        v0 = v1;
-        v1 = v2;
-        v2 = v3;
-      }
+      column(cw + dx, len, n, r2, wpos, true);
+      n += 2 * len + 1;
     }
   }
   if (x >= R.x1) return;
