@@ -273,8 +273,10 @@ def main() -> int:
     passes = max(k_n // spp, 1)
     avg_launch_s = (k_ms / 1e3) / passes
     # algorithmic bytes per launch = 16 B per node-update x node-updates of one launch
-    # + 8 B per node when the fast test mode reads its precomputed L_h[W0]
-    bytes_node = BYTES_PER_NODE + (8.0 if args.test_mode and info.kernel == N.KERNEL_FAST else 0.0)
+    # + 8 B per node and launch when the fast test mode reads its precomputed
+    # L_h[W0] (once per pass: 8 / steps_per_pass per node-update)
+    bytes_node = BYTES_PER_NODE + (8.0 / info.steps_per_pass
+                                   if args.test_mode and info.kernel == N.KERNEL_FAST else 0.0)
     nu_launch = local_nodes * spp
     alg_bytes = bytes_node * nu_launch
     achieved_gbs = alg_bytes / avg_launch_s / 1e9

@@ -126,9 +126,10 @@ int resolve_config(const nlh_params &p, Resolved &r) {
   r.wide = kern == NLH_KERNEL_FAST && nlh::wide_supported(E);
   r.ablate = 0;
   if (const char *ab = std::getenv("NLH_ABLATE")) r.ablate = std::atoi(ab);
-  // production fast mode advances two steps per pass; the source term of the
-  // test mode and a zero alpha (no centre fold) keep the single-step kernels
-  r.pair = kern == NLH_KERNEL_FAST && !p.test && nlh::pair_supported(E) && fold_ok && r.ablate == 0;
+  // fast mode advances two steps per pass (test mode too: the manufactured
+  // source of both steps folded into the pass); a zero alpha (no centre fold)
+  // keeps the single-step kernels
+  r.pair = kern == NLH_KERNEL_FAST && nlh::pair_supported(E) && fold_ok && r.ablate == 0;
   if (const char *pe = std::getenv("NLH_PAIR")) r.pair = r.pair && std::atoi(pe) != 0;
   r.halo = r.pair ? 2 * E : E;
   return NLH_OK;
@@ -326,7 +327,7 @@ int build_rectlists(nlh_solver *s, int kind) {
       // seg + 2E); at 4096^2 this picks 152 rows = 999 workgroups in one
       // round, the measured optimum; on large lattices several rounds of
       // shorter segments instead of one round with idle slots
-      const int per_cu = std::max(1, nlh::pair_blocks_per_cu(E, s->pair_split));
+      const int per_cu = std::max(1, nlh::pair_blocks_per_cu(E, s->p.test ? 4 : s->pair_split));
       int use_cu = s->pair_split != 0 ? std::min(per_cu, 4) : per_cu;
       // with an exchange the interior may be sized for fewer slots per CU,
       // leaving room for the bands and RCCL beside it (NLH_INT_PER_CU)
@@ -547,7 +548,7 @@ int launch_pair_lists(nlh_solver *s, const std::vector<nlh::RectList> &v, hipStr
   for (const auto &rl : v) {
     if (rl.nwork == 0) continue;
     const int rc = s->pair_ablate ? nlh::launch_pair_ablation(rl, s->sc, s->pair_ablate, st)
-                                  : nlh::launch_pair(rl, s->sc, s->pair_split, st);
+                                  : nlh::launch_pair(rl, s->sc, s->p.test ? 4 : s->pair_split, st);
     if (rc != 0) return fail(NLH_ERR_HIP, std::string("pair launch failed: ") + hipGetErrorString((hipError_t)rc));
   }
   return NLH_OK;
@@ -564,6 +565,9 @@ void set_time(nlh_solver *s, int64_t t) {
   const double arg = 2 * M_PI * (t * s->p.dt);
   s->sc.st2pi = 2 * M_PI * sin(arg);
   s->sc.ct = cos(arg);
+  const double arg2 = 2 * M_PI * ((t + 1) * s->p.dt);
+  s->sc.st2pi2 = 2 * M_PI * sin(arg2);
+  s->sc.ct2 = cos(arg2);
 }
 
 // halo exchange of the field in buffer parity k on the comm stream: pack the
@@ -668,10 +672,13 @@ int enqueue_step(nlh_solver *s, int nsteps) {
 
 int compute_lw(nlh_solver *s) {
   // L_h[W0](x) = sum_disk c*(W0~_j - W0_x)*dh^2 with the exact per-term
-  // order; the fast test-mode source is then b = -(2pi st) W0 - ct L_h[W0]
+  // order; the fast test-mode source is then b = -(2pi st) W0 - ct L_h[W0].
+  // With the two-step kernel (halo 2E) also over the block's E-wide frame:
+  // stage 1 computes u^{t+1} there
+  const int ext = s->pair ? (int)s->p.eps : 0;
   for (auto &b : s->blocks) {
     double *tmp = b.base[1];
-    if (nlh::launch_fill_w0(tmp, b.pitch, b.xl, (int)b.r.w, (int)b.r.h, (int)b.r.x0,
+    if (nlh::launch_fill_w0(tmp, b.pitch, b.xl, (int)b.r.w, (int)b.r.h, s->halo, (int)b.r.x0,
                             (int)b.r.y0, s->sc, s->s_main))
       return fail(NLH_ERR_HIP, "fill_w0 launch");
     nlh::RectList rl{};
@@ -682,9 +689,9 @@ int compute_lw(nlh_solver *s) {
     R.pitch = b.pitch;
     R.gx0 = (int32_t)b.r.x0;
     R.gy0 = (int32_t)b.r.y0;
-    R.x0 = 0; R.y0 = 0; R.x1 = (int)b.r.w; R.y1 = (int)b.r.h;
-    R.nstrip = (int)ceil_div(b.r.w, 64);
-    R.nseg = (int)ceil_div(b.r.h, 4);
+    R.x0 = -ext; R.y0 = -ext; R.x1 = (int)b.r.w + ext; R.y1 = (int)b.r.h + ext;
+    R.nstrip = (int)ceil_div(R.x1 - R.x0, 64);
+    R.nseg = (int)ceil_div(R.y1 - R.y0, 4);
     rl.nwork = R.nstrip * R.nseg;
     if (nlh::launch_exact_sum(rl, s->sc, s->s_main)) return fail(NLH_ERR_HIP, "L_h[W0] launch");
     HIP_TRY(hipMemsetAsync(b.base[1], 0, b.pitch * b.rows * sizeof(double), s->s_main));

@@ -62,6 +62,8 @@ struct StepConst {
   const double *wt;
   const double *qj;
   double jsum;
+  double st2pi2;   // st2pi, ct at time t+1 (two-step test mode: the second step's source)
+  double ct2;
 };
 
 // Strided rectangle copy (halo exchange: local block->block copies, pack to
@@ -122,9 +124,10 @@ int launch_copies(const CopyList &cl, void *stream);
 // u(x,y) = sxt[gx]*syt[gy] on the block interior; halo untouched.
 int launch_init_test(double *u, int64_t pitch, int32_t bx, int32_t by,
                      int32_t gx0, int32_t gy0, const StepConst &c, void *stream);
-// W0 over the padded block INCLUDING halo: sxt*syt inside the domain, 0 out.
+// W0 over the padded block INCLUDING its `halo` rows: sxt*syt inside the
+// domain, 0 out.
 int launch_fill_w0(double *u, int64_t pitch, int32_t xl, int32_t bx,
-                   int32_t by, int32_t gx0, int32_t gy0, const StepConst &c,
+                   int32_t by, int32_t halo, int32_t gx0, int32_t gy0, const StepConst &c,
                    void *stream);
 // Partial L2/Linf per workgroup into `out` (nwg entries); returns nwg.
 int norm_workgroups(int32_t bx, int32_t by);

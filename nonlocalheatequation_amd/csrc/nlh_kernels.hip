@@ -370,12 +370,12 @@ __global__ __launch_bounds__(256) void k_init_test(double *u, int64_t pitch,
 
 // W0 over the whole padded block (halo included), 0 outside the domain
 __global__ __launch_bounds__(256) void k_fill_w0(double *u, int64_t pitch,
-                                                 int xl, int rows, int gx0,
+                                                 int xl, int rows, int halo, int gx0,
                                                  int gy0, StepConst C) {
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (e >= pitch * rows) return;
   const int px = (int)(e % pitch), py = (int)(e / pitch);
-  const int gx = gx0 + px - xl, gy = gy0 + py - C.E;
+  const int gx = gx0 + px - xl, gy = gy0 + py - halo;
   const bool in = gx >= 0 && gx < C.nx && gy >= 0 && gy < C.ny;
   u[e] = in ? C.sxt[gx + C.E] * C.syt[gy + C.E] : 0.0;
 }
@@ -656,13 +656,13 @@ int launch_init_test(double *u, int64_t pitch, int32_t bx, int32_t by,
   return check_launch();
 }
 
-int launch_fill_w0(double *u, int64_t pitch, int32_t xl, int32_t bx, int32_t by,
+int launch_fill_w0(double *u, int64_t pitch, int32_t xl, int32_t bx, int32_t by, int32_t halo,
                    int32_t gx0, int32_t gy0, const StepConst &c, void *stream) {
   (void)bx;
-  const int rows = by + 2 * c.E;
+  const int rows = by + 2 * halo;
   const int64_t n = pitch * rows;
   hipLaunchKernelGGL(k_fill_w0, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, u, pitch, xl, rows, gx0, gy0, c);
+                     (hipStream_t)stream, u, pitch, xl, rows, halo, gx0, gy0, c);
   return check_launch();
 }
 

@@ -275,7 +275,16 @@ __global__ __launch_bounds__(64, (E <= 9 ? 2 : 1)) void k_pair(RectList L, StepC
 // measured best, see nlh_api.cpp); one barrier per B rows lets per-row
 // jitter of the two waves average out.  Same arithmetic and order as
 // k_pair: bitwise equal results.
-template <int E, int D, int ABL = 0, int B = kPairSplitB>
+//
+// TEST (manufactured source, sum_local_test :235-252, in the fast form
+// b(x,t) = -(2 pi st_t) W0(x) - ct_t L_h[W0](x) with the precomputed plane
+// L_h[W0] of k_fast): wave 1 also DMAs, with u^t row i, the L_h[W0] row and
+// the sin(2 pi y dh) entry of u^{t+1} row i-2E.  Stage 1 adds dt*b(t) to
+// u^{t+1} and writes (dt/alpha)*b(t+1) beside it into a second 2B-row ring;
+// stage 2 folds that into the centre accumulator of the same row, so
+// u^{t+2} = alpha*(S + kc u^{t+1} + (dt/alpha) b(t+1)).  L_h[W0] is read once
+// per two steps.
+template <int E, int D, int ABL = 0, int B = kPairSplitB, bool TEST = false>
 __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) {
   constexpr int R = 2;
   constexpr int P = 2 * E + 1;
@@ -289,12 +298,22 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
   constexpr int G = (NCH + 63) / 64;
   constexpr int U1W = W1 + 2 * E + 2;
   constexpr int U1R = 2 * B;            // u^{t+1} ring rows
+  // TEST: L_h[W0] row of the stage-1 columns x0-E .. x0-E+W1-1, staged from
+  // the even column at or before x0-E (16-byte DMA chunks)
+  constexpr int LOFF = E & 1;
+  constexpr int NCHL = TEST ? (W1 + LOFF + 1) / 2 : 0;
+  constexpr int LWW = 2 * NCHL;
+  constexpr int GT = TEST ? (NCHL + 63) / 64 + 1 : 0;  // + the sin(2 pi y dh) pair
+  constexpr int GA = G + GT;            // DMA instructions per row
   static_assert((B & (B - 1)) == 0, "B must be a power of two");
-  static_assert(D * G + D + 1 < 64, "vmcnt range");
+  static_assert(D * GA + D + 1 < 64, "vmcnt range");
   static_assert(WO >= 64, "strip too narrow for this eps");
 
-  __shared__ __attribute__((aligned(16))) double ring[K * RW + U1R * U1W];
+  __shared__ __attribute__((aligned(16))) double ring[K * RW + U1R * U1W + (TEST ? U1R * U1W + K * LWW + 2 * K : 0)];
   double *const u1buf = ring + K * RW;
+  double *const qbuf = u1buf + U1R * U1W;  // TEST: (dt/alpha) b(t+1) of the u^{t+1} rows
+  double *const lwr = qbuf + U1R * U1W;    // TEST: L_h[W0] rows, slots of the u^t ring
+  double *const syr = lwr + K * LWW;       // TEST: sin(2 pi y dh) pairs, same slots
 
   const int lane = (int)(threadIdx.x & 63);
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -316,6 +335,14 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
   const int64_t stride = up ? -pitch : pitch;
   const double alpha = C.alpha, kc = C.kc;
   const int ydir = up ? -1 : 1;
+  // TEST: block row of u^{t+1} row m (clamped to the rows a segment computes)
+  // and the sin(2 pi y dh) table index of that row
+  const int nm = n_in - 2 * E;
+  auto m_row = [&](int m) {
+    m = min(max(m, 0), nm - 1);
+    return up ? (Y1 + E - 1 - m) : (Y0 - E + m);
+  };
+  auto sy_idx = [&](int m) { return min(max(rgy0 + m_row(m) + E, 0), (int)C.ny + 2 * E - 1); };
 
   // s_barrier with every LDS access of this wave completed first; the asm
   // "memory" clobber also keeps the compiler from moving LDS accesses across
@@ -350,12 +377,14 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
     // ---- stage 1 on u^t row i
     const int gny = (int)C.ny;
     const int gy1first = rgy0 + (up ? (Y1 + E - 1) : (Y0 - E));
-    double mcol[R];
+    double mcol[R], sxv[R];
 #pragma unroll
     for (int c = 0; c < R; ++c) {
       const int gx = rgx0 + x0 - E + R * lane + c;
       mcol[c] = (gx >= 0 && gx < (int)C.nx) ? alpha : 0.0;
+      sxv[c] = TEST ? C.sxt[min(max(gx, -E), (int)C.nx + E - 1) + E] : 0.0;
     }
+    const double qs = TEST ? C.dt / alpha : 0.0;
     row_barrier();  // prologue: rows 0 .. B-1 landed
     int bs = 0;     // b % K
     for (int b = 0; b < n_in; b += P) {
@@ -373,6 +402,20 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
           const int gy = gy1first + ydir * m;
           double v0 = mcol[0] * acc[0][so];
           double v1 = mcol[1] * acc[1][so];
+          double q0 = 0.0, q1 = 0.0;
+          if constexpr (TEST) {
+            const int slot = (bs + q) & (K - 1);  // u^t row i: its L_h[W0] / sin rows
+            const double syv = syr[2 * slot + (sy_idx(m) & 1)];
+            const double *lrow = lwr + slot * LWW + LOFF + R * lane;
+            const double w00 = sxv[0] * syv, w01 = sxv[1] * syv;
+            const double lw0 = lrow[0], lw1 = lrow[1];
+            v0 = fma(-(C.st2pi * w00) - C.ct * lw0, C.dt, v0);
+            v1 = fma(-(C.st2pi * w01) - C.ct * lw1, C.dt, v1);
+            q0 = qs * (-(C.st2pi2 * w00) - C.ct2 * lw0);
+            q1 = qs * (-(C.st2pi2 * w01) - C.ct2 * lw1);
+            if (mcol[0] == 0.0) v0 = 0.0;  // columns outside the lattice
+            if (mcol[1] == 0.0) v1 = 0.0;
+          }
           if (gy < 0 || gy >= gny) {
             v0 = 0.0;
             v1 = 0.0;
@@ -381,6 +424,8 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
             asm volatile("" ::"v"(v0), "v"(v1));  // ablation: no u^{t+1} LDS write
           else
             *reinterpret_cast<double2 *>(u1buf + (m & (U1R - 1)) * U1W + R * lane) = make_double2(v0, v1);
+          if constexpr (TEST)
+            *reinterpret_cast<double2 *>(qbuf + (m & (U1R - 1)) * U1W + R * lane) = make_double2(q0, q1);
         }
         if constexpr ((ABL & 40) != 40)
           if ((i & (B - 1)) == B - 1) row_barrier();
@@ -396,7 +441,21 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
     const double *gnext = Rc.u + (int64_t)yfirst * pitch + (x0 - 2 * E);
     const uint32_t lring = __builtin_amdgcn_readfirstlane(lds_addr(ring));
     int row = 0;  // next u^t row to fetch (clamped at the last one)
+    int irow = 0;  // u^t row index of the next issue (unclamped; TEST rows follow it)
+    const double *lw0p = TEST ? Rc.lw + (x0 - E - LOFF) : nullptr;
+    const uint32_t llw = __builtin_amdgcn_readfirstlane(lds_addr(lwr));
+    const uint32_t lsy = __builtin_amdgcn_readfirstlane(lds_addr(syr));
     auto issue = [&](int slot) {
+      if constexpr (TEST) {
+        // L_h[W0] and sin(2 pi y dh) of u^{t+1} row irow - 2E (stage 1's output
+        // when it reads u^t row irow)
+        const int m = irow - 2 * E;
+        if (!(ABL & 2) && !(ABL & 256)) {
+          dma_chunks<NCHL, false, false>(lw0p + (int64_t)m_row(m) * pitch, llw + slot * LWW * 8, lane);
+          dma_chunks<1, false, false>(C.syt + (sy_idx(m) & ~1), lsy + slot * 16, lane);
+        }
+        ++irow;
+      }
       // default-policy (temporal) DMA: a strip's 2E halo columns are read
       // again by its neighbours on the same XCD (L2 hits); nt loads measured
       // 1-3% slower here (profiles/r02/pair_bench_5.jsonl); ABL 1024 = nt
@@ -411,7 +470,7 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
     };
 #pragma unroll
     for (int s = 0; s < DT; ++s) issue(s);
-    wait_vmcnt<D * G>();  // rows 0 .. B-1 landed (D rows may still fly)
+    wait_vmcnt<D * GA>();  // rows 0 .. B-1 landed (D rows may still fly)
     row_barrier();
     const int xo = x0 + R * lane;
     const bool emit0 = R * lane < WO && xo < rx1;
@@ -430,9 +489,9 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
         return;
       }
       if (j - D >= 4 * E + B)
-        wait_vmcnt<D * G + D + 1>();
+        wait_vmcnt<D * GA + D + 1>();
       else
-        wait_vmcnt<D * G>();
+        wait_vmcnt<D * GA>();
       row_barrier();
     };
     // iterations 0 .. P-1 have no u^{t+1} row yet (m2 < 0; n_in > P always):
@@ -459,6 +518,11 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
         double w2[NW];
         window(u1buf + (m2 & (U1R - 1)) * U1W + R * lane, w2);
         pair_scatter<E, q2>(w2, acc, kc);
+        if constexpr (TEST) {  // (dt/alpha) b(t+1) at the centre row of the output
+          const double *qr = qbuf + (m2 & (U1R - 1)) * U1W + R * lane + E;
+          acc[0][q2] += qr[0];
+          acc[1][q2] += qr[1];
+        }
         if ((ABL & 32) != 0 || m2 >= 2 * E) {
           const double o0 = alpha * acc[0][so];
           const double o1 = alpha * acc[1][so];
@@ -860,11 +924,15 @@ int launch_pair_abl(const RectList &rl, const StepConst &c, hipStream_t st) {
 
 // resident k_pair workgroups per CU (register/LDS-limited), for the
 // host's choice of segment height
+// variant: 0 k_pair, 1 k_pair_split, 2 k_pair_mw, 3 k_pair_pf, 4 k_pair_split
+// with the manufactured source (test mode)
 template <int E>
 int pair_blocks_per_cu_e(int variant) {
   int n = 0;
   const hipError_t e =
-      variant == 3 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_pair_pf<E, kPairSplitD>, 128, 0)
+      variant == 4 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                         &n, k_pair_split<E, kPairSplitD, 0, kPairSplitB, true>, 128, 0)
+      : variant == 3 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_pair_pf<E, kPairSplitD>, 128, 0)
       : variant == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_pair_mw<E, kPairMwD>, 192, 0)
       : variant == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_pair_split<E, kPairSplitD>, 128, 0)
                      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_pair<E, kPairD>, 64, 0);
@@ -873,7 +941,10 @@ int pair_blocks_per_cu_e(int variant) {
 
 template <int E>
 int launch_pair_e(const RectList &rl, const StepConst &c, int variant, hipStream_t st) {
-  if (variant == 3)
+  if (variant == 4)
+    hipLaunchKernelGGL((k_pair_split<E, kPairSplitD, 0, kPairSplitB, true>), dim3(rl.nwork), dim3(128), 0, st,
+                       rl, c);
+  else if (variant == 3)
     hipLaunchKernelGGL((k_pair_pf<E, kPairSplitD>), dim3(rl.nwork), dim3(128), 0, st, rl, c);
   else if (variant == 2)
     hipLaunchKernelGGL((k_pair_mw<E, kPairMwD>), dim3(rl.nwork), dim3(192), 0, st, rl, c);

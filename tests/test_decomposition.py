@@ -206,11 +206,12 @@ def test_block_plan_covers_lattice():
         assert (cover == 1).all()
 
 
-@pytest.mark.parametrize("kernel,test,width", [("exact", False, 1), ("auto", True, 1), ("auto", False, 2)])
+@pytest.mark.parametrize("kernel,test,width", [("exact", False, 1), ("exact", True, 1), ("auto", True, 2),
+                                               ("auto", False, 2)])
 def test_halo_plan_covers_halo_exactly(kernel, test, width):
     """The plan's pieces fill exactly the halo frame of each block: eps wide
-    for the single-step kernels (exact, and the fast test mode), 2*eps for the
-    two-step production pass -- the width nlh_create resolves."""
+    for the single-step kernels (exact), 2*eps for the two-step pass of the
+    fast mode (production and test mode) -- the width nlh_create resolves."""
     nx, ny, eps, tiles, world = 60, 48, 7, (6, 4), 3
     kw = dict(k=1.0, dt=eps ** 4 / (nx * nx * 8.0 * N.disk_count(eps)), dh=1.0 / nx, test=test, kernel=kernel)
     H = width * eps

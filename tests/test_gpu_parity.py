@@ -270,6 +270,53 @@ def test_pair_pass_matches_oracle(oracle, monkeypatch, eps, nt):
     assert np.max(np.abs(u1 - u_ref)) <= 1e-12 * scale
 
 
+@pytest.mark.parametrize("eps", [1, 3, 5, 8, 12, 16])
+@pytest.mark.parametrize("nt", [2, 5, 8])
+def test_pair_test_mode_matches_oracle(oracle, monkeypatch, eps, nt):
+    """Two-step pass with the manufactured source (test mode): b(t) added in
+    stage 1, (dt/alpha) b(t+1) folded into stage 2's centre accumulator; odd nt
+    ends with one single k_fast step.  Per node vs the oracle, the L2 and
+    L-inf error outputs, and vs the single-step test-mode kernel."""
+    nx, ny = 301, 203
+    r = N.BatchRow(nx, ny, nt, eps, 1.0, 0.0, 1.0 / nx)
+    r.dt = 0.7 * eps ** 4 * r.dh ** 2 / (8 * r.k * N.disk_count(eps))
+    u_ref, l2_ref, li_ref = _oracle_run(oracle, r, True)
+    scale = np.max(np.abs(u_ref))
+    u, l2, li, info = _gpu_run(r, True, "auto")
+    assert info.steps_per_pass == 2 and info.pass_kernel == "k_pair_split"
+    assert np.max(np.abs(u - u_ref)) <= 1e-12 * scale
+    n = nx * ny
+    d = np.max(np.abs(u - u_ref))
+    assert abs(l2 - l2_ref) <= 1e-10 * l2_ref + d * (2 * np.sqrt(n * l2_ref) + n * d)
+    assert abs(li - li_ref) <= 1e-9 * li_ref + d
+    monkeypatch.setenv("NLH_PAIR", "0")
+    u1, _, _, info1 = _gpu_run(r, True, "auto")
+    assert info1.steps_per_pass == 1
+    assert np.max(np.abs(u1 - u)) <= 1e-12 * scale
+
+
+def test_pair_test_mode_multiblock(oracle, monkeypatch):
+    """Test mode through the two-step pass on 3 x 2 blocks over RCCL (to
+    self): the L_h[W0] plane is computed on each block's E-wide frame too."""
+    monkeypatch.setenv("NLH_RCCL_SELF", "1")
+    nx, ny, eps, nt = 192, 128, 6, 6
+    r = N.BatchRow(nx, ny, nt, eps, 1.0, 0.0, 1.0 / nx)
+    r.dt = 0.7 * eps ** 4 * r.dh ** 2 / (8 * r.k * N.disk_count(eps))
+    u_ref, l2_ref, _ = _oracle_run(oracle, r, True)
+    with N.Solver(nx, ny, eps, r.k, r.dt, r.dh, test=True, kernel="auto", tiles=(3, 2), split_tiles=True) as s:
+        s.test_init()
+        s.run(nt)
+        s.synchronize()
+        u = s.field()
+        l2, _ = s.errors(nt)
+        info = s.info()
+    assert info.nblocks == 6 and info.steps_per_pass == 2
+    d = np.max(np.abs(u - u_ref))
+    assert d <= 1e-12 * np.max(np.abs(u_ref))
+    n = nx * ny
+    assert abs(l2 - l2_ref) <= 1e-10 * l2_ref + d * (2 * np.sqrt(n * l2_ref) + n * d)
+
+
 @pytest.mark.parametrize("seg", [1, 7, 40, 1000])
 def test_pair_segment_heights(oracle, seg):
     """Segment heights from one row to a whole-strip sweep (seg_rows override)."""
