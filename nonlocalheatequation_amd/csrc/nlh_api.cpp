@@ -199,6 +199,7 @@ struct nlh_solver {
   int ablate = 0;     // diagnostics only (NLH_ABLATE), never set in production
   int pair_ablate = 0;  // diagnostics only (NLH_PAIR_ABLATE)
   int pair_split = 1;  // 1 k_pair_split (default), 0 k_pair, 2 k_pair_mw, 3 k_pair_pf (NLH_PAIR_SPLIT)
+  int pair_test = 4;   // test-mode pass: 4 k_pair_split<TEST> D=8 B=4, 5 D=4 B=2 (NLH_PAIR_TEST=1)
   hipStream_t s_main = nullptr, s_comm = nullptr, s_band = nullptr;
   hipEvent_t ev_ready = nullptr, ev_halo = nullptr, ev_band = nullptr, ev_int = nullptr;
   bool halo_fresh = false;  // the current field's halo holds its neighbours' values
@@ -327,7 +328,7 @@ int build_rectlists(nlh_solver *s, int kind) {
       // seg + 2E); at 4096^2 this picks 152 rows = 999 workgroups in one
       // round, the measured optimum; on large lattices several rounds of
       // shorter segments instead of one round with idle slots
-      const int per_cu = std::max(1, nlh::pair_blocks_per_cu(E, s->p.test ? 4 : s->pair_split));
+      const int per_cu = std::max(1, nlh::pair_blocks_per_cu(E, s->p.test ? s->pair_test : s->pair_split));
       int use_cu = s->pair_split != 0 ? std::min(per_cu, 4) : per_cu;
       // with an exchange the interior may be sized for fewer slots per CU,
       // leaving room for the bands and RCCL beside it (NLH_INT_PER_CU)
@@ -548,7 +549,7 @@ int launch_pair_lists(nlh_solver *s, const std::vector<nlh::RectList> &v, hipStr
   for (const auto &rl : v) {
     if (rl.nwork == 0) continue;
     const int rc = s->pair_ablate ? nlh::launch_pair_ablation(rl, s->sc, s->pair_ablate, st)
-                                  : nlh::launch_pair(rl, s->sc, s->p.test ? 4 : s->pair_split, st);
+                                  : nlh::launch_pair(rl, s->sc, s->p.test ? s->pair_test : s->pair_split, st);
     if (rc != 0) return fail(NLH_ERR_HIP, std::string("pair launch failed: ") + hipGetErrorString((hipError_t)rc));
   }
   return NLH_OK;
@@ -812,6 +813,7 @@ int create_impl(const nlh_params *pin, nlh_solver *s, ncclComm_t reuse_comm = nu
   if (const char *cp = std::getenv("NLH_COMM_PRIO"))
     if (std::atoi(cp) != 0) HIP_TRY(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
   if (const char *ps = std::getenv("NLH_PAIR_SPLIT")) s->pair_split = std::min(3, std::max(0, std::atoi(ps)));
+  if (const char *pt = std::getenv("NLH_PAIR_TEST")) s->pair_test = std::atoi(pt) == 1 ? 5 : 4;
   if (s->pair_ablate >= 10000) s->pair_split = 1;
   s->halo = rv.halo;
   s->plan = nlh::make_plan(p.nx, p.ny, s->halo, tx, ty, s->owner, p.split_tiles == 0);

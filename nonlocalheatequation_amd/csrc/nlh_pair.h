@@ -932,6 +932,7 @@ int pair_blocks_per_cu_e(int variant) {
   const hipError_t e =
       variant == 4 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
                          &n, k_pair_split<E, kPairSplitD, 0, kPairSplitB, true>, 128, 0)
+      : variant == 5 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_pair_split<E, 4, 0, 2, true>, 128, 0)
       : variant == 3 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_pair_pf<E, kPairSplitD>, 128, 0)
       : variant == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_pair_mw<E, kPairMwD>, 192, 0)
       : variant == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_pair_split<E, kPairSplitD>, 128, 0)
@@ -944,6 +945,8 @@ int launch_pair_e(const RectList &rl, const StepConst &c, int variant, hipStream
   if (variant == 4)
     hipLaunchKernelGGL((k_pair_split<E, kPairSplitD, 0, kPairSplitB, true>), dim3(rl.nwork), dim3(128), 0, st,
                        rl, c);
+  else if (variant == 5)  // test mode, 8-slot rings (more workgroups per CU)
+    hipLaunchKernelGGL((k_pair_split<E, 4, 0, 2, true>), dim3(rl.nwork), dim3(128), 0, st, rl, c);
   else if (variant == 3)
     hipLaunchKernelGGL((k_pair_pf<E, kPairSplitD>), dim3(rl.nwork), dim3(128), 0, st, rl, c);
   else if (variant == 2)
