@@ -199,7 +199,10 @@ struct nlh_solver {
   int ablate = 0;     // diagnostics only (NLH_ABLATE), never set in production
   int pair_ablate = 0;  // diagnostics only (NLH_PAIR_ABLATE)
   int pair_split = 1;  // 1 k_pair_split (default), 0 k_pair, 2 k_pair_mw, 3 k_pair_pf (NLH_PAIR_SPLIT)
-  int pair_test = 4;   // test-mode pass: 4 k_pair_split<TEST> D=8 B=4, 5 D=4 B=2 (NLH_PAIR_TEST=1)
+  // test-mode pass: 5 = k_pair_split<TEST> with 8-slot rings (D=4, B=2; 322 vs
+  // 287 G node/s at C2 for the production rings, profiles/r02/tune_test.jsonl),
+  // 4 = D=8, B=4 (NLH_PAIR_TEST=0)
+  int pair_test = 5;
   hipStream_t s_main = nullptr, s_comm = nullptr, s_band = nullptr;
   hipEvent_t ev_ready = nullptr, ev_halo = nullptr, ev_band = nullptr, ev_int = nullptr;
   bool halo_fresh = false;  // the current field's halo holds its neighbours' values
@@ -813,7 +816,7 @@ int create_impl(const nlh_params *pin, nlh_solver *s, ncclComm_t reuse_comm = nu
   if (const char *cp = std::getenv("NLH_COMM_PRIO"))
     if (std::atoi(cp) != 0) HIP_TRY(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
   if (const char *ps = std::getenv("NLH_PAIR_SPLIT")) s->pair_split = std::min(3, std::max(0, std::atoi(ps)));
-  if (const char *pt = std::getenv("NLH_PAIR_TEST")) s->pair_test = std::atoi(pt) == 1 ? 5 : 4;
+  if (const char *pt = std::getenv("NLH_PAIR_TEST")) s->pair_test = std::atoi(pt) == 0 ? 4 : 5;
   if (s->pair_ablate >= 10000) s->pair_split = 1;
   s->halo = rv.halo;
   s->plan = nlh::make_plan(p.nx, p.ny, s->halo, tx, ty, s->owner, p.split_tiles == 0);

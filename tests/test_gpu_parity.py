@@ -289,6 +289,9 @@ def test_pair_test_mode_matches_oracle(oracle, monkeypatch, eps, nt):
     d = np.max(np.abs(u - u_ref))
     assert abs(l2 - l2_ref) <= 1e-10 * l2_ref + d * (2 * np.sqrt(n * l2_ref) + n * d)
     assert abs(li - li_ref) <= 1e-9 * li_ref + d
+    monkeypatch.setenv("NLH_PAIR_TEST", "0")  # the production-sized rings (D=8, B=4)
+    u4, _, _, _ = _gpu_run(r, True, "auto")
+    assert np.max(np.abs(u4 - u_ref)) <= 1e-12 * scale
     monkeypatch.setenv("NLH_PAIR", "0")
     u1, _, _, info1 = _gpu_run(r, True, "auto")
     assert info1.steps_per_pass == 1
