@@ -203,6 +203,7 @@ struct nlh_solver {
   // 287 G node/s at C2 for the production rings, profiles/r02/tune_test.jsonl),
   // 4 = D=8, B=4 (NLH_PAIR_TEST=0)
   int pair_test = 5;
+  int pair_cu = 4;     // split-kernel workgroups per CU the segments are sized for (NLH_PAIR_CU)
   hipStream_t s_main = nullptr, s_comm = nullptr, s_band = nullptr;
   hipEvent_t ev_ready = nullptr, ev_halo = nullptr, ev_band = nullptr, ev_int = nullptr;
   bool halo_fresh = false;  // the current field's halo holds its neighbours' values
@@ -332,7 +333,7 @@ int build_rectlists(nlh_solver *s, int kind) {
       // round, the measured optimum; on large lattices several rounds of
       // shorter segments instead of one round with idle slots
       const int per_cu = std::max(1, nlh::pair_blocks_per_cu(E, s->p.test ? s->pair_test : s->pair_split));
-      int use_cu = s->pair_split != 0 ? std::min(per_cu, 4) : per_cu;
+      int use_cu = s->pair_split != 0 ? std::min(per_cu, s->pair_cu) : per_cu;
       // with an exchange the interior may be sized for fewer slots per CU,
       // leaving room for the bands and RCCL beside it (NLH_INT_PER_CU)
       // -- measured a win up to 4096^2-sized blocks (166 vs 182 us/step for
@@ -815,7 +816,11 @@ int create_impl(const nlh_params *pin, nlh_solver *s, ncclComm_t reuse_comm = nu
   int prio_lo = 0, prio_hi = 0;  // NLH_COMM_PRIO=1: exchange + band streams at the highest priority
   if (const char *cp = std::getenv("NLH_COMM_PRIO"))
     if (std::atoi(cp) != 0) HIP_TRY(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
-  if (const char *ps = std::getenv("NLH_PAIR_SPLIT")) s->pair_split = std::min(3, std::max(0, std::atoi(ps)));
+  if (const char *ps = std::getenv("NLH_PAIR_SPLIT")) {
+    const int v = std::min(4, std::max(0, std::atoi(ps)));
+    s->pair_split = v == 4 ? 6 : v;  // 4: k_pair_split with 8-slot rings (variant 6)
+  }
+  if (const char *pc = std::getenv("NLH_PAIR_CU")) s->pair_cu = std::max(1, std::atoi(pc));
   if (const char *pt = std::getenv("NLH_PAIR_TEST")) s->pair_test = std::atoi(pt) == 0 ? 4 : 5;
   if (s->pair_ablate >= 10000) s->pair_split = 1;
   s->halo = rv.halo;
@@ -1413,7 +1418,7 @@ int nlh_get_info(const nlh_solver *s, nlh_info *info) {
   info->steps_per_pass = s->pair ? 2 : 1;
   info->owners = s->owners;
   const char *pk = s->pair ? (s->pair_split == 3 ? "k_pair_pf" : s->pair_split == 2 ? "k_pair_mw"
-                              : s->pair_split == 1 ? "k_pair_split" : "k_pair")
+                              : (s->pair_split == 1 || s->pair_split == 6) ? "k_pair_split" : "k_pair")
                            : s->wide ? "k_wide" : s->weighted ? "k_weighted"
                            : s->kernel == NLH_KERNEL_FAST ? "k_fast"
                            : nlh::exact_lds_ok((int)s->p.eps, s->p.test != 0) ? "k_exact_lds" : "k_exact";

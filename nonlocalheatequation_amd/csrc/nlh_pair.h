@@ -933,6 +933,7 @@ int pair_blocks_per_cu_e(int variant) {
       variant == 4 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(
                          &n, k_pair_split<E, kPairSplitD, 0, kPairSplitB, true>, 128, 0)
       : variant == 5 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_pair_split<E, 4, 0, 2, true>, 128, 0)
+      : variant == 6 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_pair_split<E, 4, 0, 2>, 128, 0)
       : variant == 3 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_pair_pf<E, kPairSplitD>, 128, 0)
       : variant == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_pair_mw<E, kPairMwD>, 192, 0)
       : variant == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_pair_split<E, kPairSplitD>, 128, 0)
@@ -947,6 +948,8 @@ int launch_pair_e(const RectList &rl, const StepConst &c, int variant, hipStream
                        rl, c);
   else if (variant == 5)  // test mode, 8-slot rings (more workgroups per CU)
     hipLaunchKernelGGL((k_pair_split<E, 4, 0, 2, true>), dim3(rl.nwork), dim3(128), 0, st, rl, c);
+  else if (variant == 6)  // production, 8-slot rings (diagnostics: NLH_PAIR_SPLIT=4)
+    hipLaunchKernelGGL((k_pair_split<E, 4, 0, 2>), dim3(rl.nwork), dim3(128), 0, st, rl, c);
   else if (variant == 3)
     hipLaunchKernelGGL((k_pair_pf<E, kPairSplitD>), dim3(rl.nwork), dim3(128), 0, st, rl, c);
   else if (variant == 2)
