@@ -174,6 +174,8 @@ struct Flag {
   operator bool() const { return v.load(); }
 };
 
+constexpr size_t kEvFold = 4096;  // timing events kept before folding (nlh_run)
+
 struct Peer {
   int rank = 0;
   int64_t send_count = 0, recv_count = 0;  // doubles
@@ -246,6 +248,10 @@ struct nlh_solver {
   std::vector<hipEvent_t> ev_pool;
   size_t ev_used = 0;
   std::vector<int> ev_steps;  // time steps covered by each timed event pair
+  // pairs already folded into a running total (long busy windows: the pool
+  // is drained every kEvFold events instead of growing with the run)
+  double ev_acc_ms = 0.0;
+  int64_t ev_acc_steps = 0;
   int64_t device_bytes = 0;
   char arch[32] = {0};
   // logging snapshots (nlh_snapshot_begin / _wait): owned nodes packed block
@@ -1116,6 +1122,22 @@ int repartition_impl(nlh_solver *s, const std::vector<int32_t> &own) {
   return NLH_OK;
 }
 
+// sum the recorded event pairs into the running total and recycle the pool
+int fold_events(nlh_solver *s) {
+  HIP_TRY(hipStreamSynchronize(s->s_main));
+  HIP_TRY(hipStreamSynchronize(s->s_comm));
+  HIP_TRY(hipStreamSynchronize(s->s_band));
+  for (size_t i = 0; i + 1 < s->ev_used; i += 2) {
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, s->ev_pool[i], s->ev_pool[i + 1]));
+    s->ev_acc_ms += ms;
+  }
+  for (int n : s->ev_steps) s->ev_acc_steps += n;
+  s->ev_used = 0;
+  s->ev_steps.clear();
+  return NLH_OK;
+}
+
 // this rank's busy milliseconds since busy timing was enabled
 int local_busy(nlh_solver *s, double &ms) {
   int64_t steps = 0;
@@ -1327,6 +1349,7 @@ int nlh_run(nlh_solver *s, int64_t nsteps) {
   int rc = set_device(s);
   if (rc) return rc;
   if (nsteps == 0) return NLH_OK;
+  if (s->timing != 0 && s->ev_used >= kEvFold && (rc = fold_events(s))) return rc;
   // timing: one event pair on the stencil stream around the whole call, so
   // back-to-back passes are not separated by per-launch event records
   hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -1437,6 +1460,8 @@ int nlh_kernel_timing(nlh_solver *s, int enable) {
   s->timing = enable == 2 ? 2 : enable != 0 ? 1 : 0;
   s->ev_used = 0;
   s->ev_steps.clear();
+  s->ev_acc_ms = 0.0;
+  s->ev_acc_steps = 0;
   return NLH_OK;
 }
 
@@ -1447,14 +1472,14 @@ int nlh_kernel_time(nlh_solver *s, double *total_ms, int64_t *steps_out) {
   HIP_TRY(hipStreamSynchronize(s->s_main));
   HIP_TRY(hipStreamSynchronize(s->s_comm));
   HIP_TRY(hipStreamSynchronize(s->s_band));
-  double tot = 0.0;
+  double tot = s->ev_acc_ms;
   for (size_t i = 0; i + 1 < s->ev_used; i += 2) {
     float ms = 0.f;
     HIP_TRY(hipEventElapsedTime(&ms, s->ev_pool[i], s->ev_pool[i + 1]));
     tot += ms;
   }
   *total_ms = tot;
-  int64_t steps = 0;
+  int64_t steps = s->ev_acc_steps;
   for (int n : s->ev_steps) steps += n;
   *steps_out = steps;
   return NLH_OK;
