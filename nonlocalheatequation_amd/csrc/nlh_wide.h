@@ -71,10 +71,8 @@ __device__ __forceinline__ double tree_sum(const double (&p)[N]) {
 }
 
 // ABL (diagnostics, timing only): 1 = a scheduling barrier between rows
-// XPF: the first window group (and centre value) of row i+1 is read from LDS
-// during the last group of row i (after waiting for row i+1's DMA there)
 template <int E, int CH, bool TEST, int D = kWideD, int ABL = 0, int PIN = 1, bool AB = false, int OBP = 16,
-          bool SPLIT8 = true, bool XPF = false>
+          bool SPLIT8 = true>
 __global__ __launch_bounds__(64, 1) void k_wide(RectList L, StepConst C) {
   constexpr int W = 64;                 // output columns per strip
   constexpr int EP = (E + 1) & ~1;      // staged halo columns per side (16-B rows)
@@ -165,26 +163,6 @@ __global__ __launch_bounds__(64, 1) void k_wide(RectList L, StepConst C) {
   const double qs = TEST ? C.dt / alpha : 0.0;
   const int nchunk = (n_in + CH - 1) / CH;
   bool full = false;  // the previous chunk stored CH output rows
-  static_assert(!XPF || (SPLIT8 && !AB), "XPF reads like SPLIT8");
-  double nwl[kWideLG], nwr[kWideLG], nwc = 0.0;  // XPF: group 0 + centre of the next row
-  auto prefetch0 = [&](int irow) __attribute__((always_inline)) {
-    const double *wn = ring + (irow & (K - 1)) * RWS + (EP - E) + lane;
-    nwc = wn[E];
-    asm volatile("" ::: "memory");
-#pragma unroll
-    for (int t = 0; t < kWideLG; ++t) {
-      if (1 + t <= E) {
-        nwl[t] = wn[E - (1 + t)];
-        asm volatile("" ::: "memory");
-        nwr[t] = wn[E + (1 + t)];
-        asm volatile("" ::: "memory");
-      }
-    }
-  };
-  if constexpr (XPF) {
-    wait_vmcnt<(D - 1) * G>();  // row 0 landed
-    prefetch0(0);
-  }
   for (int j = 0; j < nchunk; ++j) {
     const int ibase = j * CH;
     auto row = [&](auto cc) __attribute__((always_inline)) {
@@ -194,9 +172,7 @@ __global__ __launch_bounds__(64, 1) void k_wide(RectList L, StepConst C) {
       issue();  // input row i + D
       // row i landed.  Issued after its DMA: the DMAs of rows i+1 .. i+D,
       // and for c < D the CH output stores of the previous chunk's end
-      // (XPF: waited for in row i-1)
-      if constexpr (XPF) {
-      } else if constexpr (c < D) {
+      if constexpr (c < D) {
         if (full)
           wait_vmcnt<D * G + CH>();
         else
@@ -267,18 +243,8 @@ __global__ __launch_bounds__(64, 1) void k_wide(RectList L, StepConst C) {
           }
         }
       };
-      double wc;
-      if constexpr (XPF) {
-        wc = nwc;
-#pragma unroll
-        for (int t = 0; t < kWideLG; ++t) {
-          wl[0][t] = nwl[t];
-          wr[0][t] = nwr[t];
-        }
-      } else {
-        wc = AB ? ((E % 2 == 0) ? wpair(E / 2).x : wpair(E / 2).y) : wrow[E];
-        load_group(std::integral_constant<int, 0>{});
-      }
+      const double wc = AB ? ((E % 2 == 0) ? wpair(E / 2).x : wpair(E / 2).y) : wrow[E];
+      load_group(std::integral_constant<int, 0>{});
       // dy = -E: first term of output a = c + 2E; dy = +E: last of a = c
       acc[c + 2 * E] = wc;
       acc[c] += wc;
@@ -290,22 +256,7 @@ __global__ __launch_bounds__(64, 1) void k_wide(RectList L, StepConst C) {
         // scheduler may not hoist later reads (register pressure) or sink
         // these adds past them
         __builtin_amdgcn_sched_barrier(0);
-        if constexpr (g + 1 < NG) {
-          load_group(std::integral_constant<int, g + 1>{});
-        } else if constexpr (XPF) {
-          // row i+1: issued after its DMA are the DMAs of rows i+2 .. i+D and,
-          // when the previous chunk ended among rows i+1-D .. i-1 (c <= D-2),
-          // its CH stores
-          if constexpr (c <= D - 2) {
-            if (full)
-              wait_vmcnt<(D - 1) * G + CH>();
-            else
-              wait_vmcnt<(D - 1) * G>();
-          } else {
-            wait_vmcnt<(D - 1) * G>();
-          }
-          prefetch0(i + 1);
-        }
+        if constexpr (g + 1 < NG) load_group(std::integral_constant<int, g + 1>{});
         // the window sum grows by p_L = w[E-L] + w[E+L] per level; it is only
         // needed at levels some output uses, so the p of the levels between
         // two used ones are summed as a tree and folded in once (the same
