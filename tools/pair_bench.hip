@@ -84,11 +84,13 @@ int main(int argc, char **argv) {
   // only (no LDS reads, no vmcnt waits, no stores, no DMA)
   std::vector<Variant> vs = {
       {"split_D8_B4", k_pair_split<E, 8, 0, 4>, 128, 4, 128 - 2 * E},
-      {"split_abl512_ntstore", k_pair_split<E, 8, 512, 4>, 128, 4, 128 - 2 * E},
-      {"split_abl1024_tDMA", k_pair_split<E, 8, 1024, 4>, 128, 4, 128 - 2 * E},
-      {"split_abl1536_ntstore_tDMA", k_pair_split<E, 8, 1536, 4>, 128, 4, 128 - 2 * E},
       {"abl_no_dma_no_store", k_pair_split<E, 8, 384, 4>, 128, 4, 128 - 2 * E},
       {"abl_valu_only", k_pair_split<E, 8, 452, 4>, 128, 4, 128 - 2 * E},
+      {"split_D8_B2", k_pair_split<E, 8, 0, 2>, 128, 4, 128 - 2 * E},
+      {"split_D6_B4", k_pair_split<E, 6, 0, 4>, 128, 4, 128 - 2 * E},
+      {"split_D4_B4", k_pair_split<E, 4, 0, 4>, 128, 4, 128 - 2 * E},
+      {"split_D4_B2", k_pair_split<E, 4, 0, 2>, 128, 4, 128 - 2 * E},
+      {"split_D4_B2_6wg", k_pair_split<E, 4, 0, 2>, 128, 6, 128 - 2 * E},
       {"split_D8_B4_seg76", k_pair_split<E, 8, 0, 4>, 128, 8, 128 - 2 * E},
       {"split_D8_B4_seg304", k_pair_split<E, 8, 0, 4>, 128, 2, 128 - 2 * E},
   };
