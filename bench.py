@@ -180,6 +180,8 @@ def main() -> int:
     ap.add_argument("--lattice", type=int, default=NB, help="lattice edge per GPU (weak) or total (--strong)")
     ap.add_argument("--strong", action="store_true")
     ap.add_argument("--test-mode", action="store_true")
+    # J(r) = 1 - r (problem_description.tex:159; not the BASELINE metric, whose J = 1)
+    ap.add_argument("--influence", default="constant", choices=["constant", "linear"])
     args = ap.parse_args()
     eps, nb = args.eps, args.lattice
 
@@ -214,6 +216,8 @@ def main() -> int:
         nx, ny = nb * px, nb * py
     dh = 1.0 / nb
     dt = eps ** 4 * dh * dh / (8.0 * N.disk_count(eps))
+    if args.influence == "linear":
+        dt /= 5.0  # c = 40 k / (eps dh)^4: five times J = 1's c, same stability margin
 
     comm_id = None
     if nranks > 1:
@@ -222,7 +226,8 @@ def main() -> int:
         comm_id = obj[0]
 
     s = N.Solver(nx, ny, eps, 1.0, dt, dh, test=args.test_mode, kernel=args.kernel, device=local,
-                 rank=rank, nranks=nranks, tiles=(px, py), comm_id=comm_id, seg_rows=args.seg_rows)
+                 rank=rank, nranks=nranks, tiles=(px, py), comm_id=comm_id, seg_rows=args.seg_rows,
+                 influence=args.influence)
     info = s.info()
     # every rank owns exactly one block of the px x py grid: the communicator
     # and the plan both see all N ranks
@@ -282,7 +287,7 @@ def main() -> int:
     achieved_gbs = alg_bytes / avg_launch_s / 1e9
     fp64_equiv_tflops = 2.0 * info.disk_points * nu_launch / avg_launch_s / 1e12
 
-    wkey = workload_key(nb, eps, args.strong, args.test_mode)
+    wkey = workload_key(nb, eps, args.strong, args.test_mode) + ("_linear" if args.influence == "linear" else "")
     pmc, pmc_path = read_pmc(kname, wkey) if nranks == 1 else (None, None)
     traffic = pmc["hbm_bytes_per_launch"] if pmc else None
     physical = None
@@ -313,7 +318,7 @@ def main() -> int:
     result = None
     if rank == 0:
         cpu = None
-        if not args.no_cpu_baseline and nranks == 1:
+        if not args.no_cpu_baseline and nranks == 1 and args.influence == "constant":
             # bounded sample: at most a 4096^2 lattice of the same eps / mode
             cpu = cpu_baseline(host_cpu_share(), min(nb, NB), eps, args.test_mode)
         result = {
@@ -332,7 +337,9 @@ def main() -> int:
             "data": "synthetic (test_init IC sin(2 pi x) sin(2 pi y); no dataset)",
             "config": {
                 "workload": workload_name(nb, eps, args.strong, args.test_mode, nx, ny)
-                            + f", {args.kernel} kernel" + (f", {px}x{py} blocks + RCCL ghost exchange" if nranks > 1 else ""),
+                            + f", {args.kernel} kernel"
+                            + (", J(r) = 1 - r" if args.influence == "linear" else "")
+                            + (f", {px}x{py} blocks + RCCL ghost exchange" if nranks > 1 else ""),
                 "lattice": [nx, ny], "eps": eps, "blocks": [px, py], "test_mode": args.test_mode,
                 "disk_points": info.disk_points, "dt": dt, "dh": dh, "kernel": args.kernel,
                 "parallelism": f"{px}x{py} block decomposition, one rank per GPU" if nranks > 1 else "1 GPU",
