@@ -282,6 +282,87 @@ __global__ __launch_bounds__(256) void k_weighted(RectList L, StepConst C) {
 }
 
 // ----------------------------------------------------------------------------
+// k_weighted_col: k_weighted's operator with the disk walked column by column
+// (dx outer, dy inner) over the same LDS tile, J(dx, |dy|) staged in LDS too.
+// Each thread owns 4 vertically adjacent nodes of one column; per dx > 0 the
+// mirror columns are summed once per tile row, p(r) = u(x+dx, r) + u(x-dx, r),
+// and a 4-value window of p slides down the column, so one pair of LDS reads
+// and one add serve a row of 4 FMAs (k_weighted: 4 reads and 3 adds per group
+// per node).  FMA order differs from k_weighted's: fast-mode tolerance.
+template <bool TEST>
+__global__ __launch_bounds__(256) void k_weighted_col(RectList L, StepConst C) {
+  extern __shared__ double tile[];
+  const int work = xcd_remap(blockIdx.x, gridDim.x);
+  const int ri = find_rect(L, work);
+  const Rect &R = L.r[ri];
+  const int local = work - R.wg_begin;
+  const int tx = local % R.nstrip, ty = local / R.nstrip;
+  const int E = C.E;
+  const int x0 = R.x0 + tx * 64, y0 = R.y0 + ty * 16;
+  const int TW = 64 + 2 * E, TH = 16 + 2 * E;
+  const int64_t p = R.pitch;
+  const int ylast = R.y1 + E - 1;  // rows past it only feed nodes that are not stored
+  double *qjs = tile + TW * TH;    // J(dx, dy), dx, dy in [0, E]
+  for (int e = (int)threadIdx.x; e < TW * TH; e += 256) {
+    const int r = e / TW, cc = e - r * TW;
+    const int gy = min(y0 - E + r, ylast);
+    tile[e] = R.u[(int64_t)gy * p + (x0 - E + cc)];
+  }
+  for (int e = (int)threadIdx.x; e < (E + 1) * (E + 1); e += 256) qjs[e] = C.qj[e];
+  __syncthreads();
+  const int lx = (int)(threadIdx.x & 63), ly = (int)(threadIdx.x >> 6) * 4;
+  const double *c = tile + (ly + E) * TW + (lx + E);  // node (x0 + lx, y0 + ly)
+  double sacc[4] = {0.0, 0.0, 0.0, 0.0};
+  // one disk column pair: rows -len .. len+3 around the 4 nodes, four dy per
+  // iteration (the window slides by renaming)
+  auto column = [&](const double *a, const double *b, bool pair, int len, const double *jr)
+      __attribute__((always_inline)) {
+    auto pv = [&](int r) __attribute__((always_inline)) {
+      return pair ? a[r * TW] + b[r * TW] : a[r * TW];
+    };
+    double v0 = pv(-len), v1 = pv(1 - len), v2 = pv(2 - len);
+    int dy = -len;
+    for (; dy + 3 <= len; dy += 4) {
+      const double v3 = pv(dy + 3), v4 = pv(dy + 4), v5 = pv(dy + 5), v6 = pv(dy + 6);
+      const double j0 = jr[abs(dy)], j1 = jr[abs(dy + 1)], j2 = jr[abs(dy + 2)], j3 = jr[abs(dy + 3)];
+      sacc[0] = fma(j0, v0, sacc[0]); sacc[1] = fma(j0, v1, sacc[1]); sacc[2] = fma(j0, v2, sacc[2]); sacc[3] = fma(j0, v3, sacc[3]);
+      sacc[0] = fma(j1, v1, sacc[0]); sacc[1] = fma(j1, v2, sacc[1]); sacc[2] = fma(j1, v3, sacc[2]); sacc[3] = fma(j1, v4, sacc[3]);
+      sacc[0] = fma(j2, v2, sacc[0]); sacc[1] = fma(j2, v3, sacc[1]); sacc[2] = fma(j2, v4, sacc[2]); sacc[3] = fma(j2, v5, sacc[3]);
+      sacc[0] = fma(j3, v3, sacc[0]); sacc[1] = fma(j3, v4, sacc[1]); sacc[2] = fma(j3, v5, sacc[2]); sacc[3] = fma(j3, v6, sacc[3]);
+      v0 = v4;
+      v1 = v5;
+      v2 = v6;
+    }
+    for (; dy <= len; ++dy) {
+      const double v3 = pv(dy + 3);
+      const double j = jr[abs(dy)];
+      sacc[0] = fma(j, v0, sacc[0]); sacc[1] = fma(j, v1, sacc[1]); sacc[2] = fma(j, v2, sacc[2]); sacc[3] = fma(j, v3, sacc[3]);
+      v0 = v1;
+      v1 = v2;
+      v2 = v3;
+    }
+  };
+  column(c, c, false, E, qjs);  // dx = 0 (len(0) = E)
+  for (int dx = 1; dx <= E; ++dx) column(c + dx, c - dx, true, C.lens[dx], qjs + dx * (E + 1));
+  const int x = x0 + lx;
+  if (x >= R.x1) return;
+  const double alpha = C.alpha, jsum = C.jsum;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int y = y0 + ly + k;
+    if (y >= R.y1) break;
+    const double uc = c[k * TW];
+    double out = fma(alpha, fma(-jsum, uc, sacc[k]), uc);
+    if (TEST) {
+      const double w0 = C.sxt[R.gx0 + x + E] * C.syt[R.gy0 + y + E];
+      const double bsrc = -(C.st2pi * w0) - C.ct * R.lw[(int64_t)y * p + x];
+      out = fma(bsrc, C.dt, out);
+    }
+    R.un[(int64_t)y * p + x] = out;
+  }
+}
+
+// ----------------------------------------------------------------------------
 // 1D solver (src/1d_nonlocal_serial.cpp): one thread per node, the
 // reference's per-term order; u has eps zero nodes on each side
 template <bool TEST>
@@ -634,6 +715,14 @@ bool weighted_supported(int E) {
 
 int launch_weighted(const RectList &rl, const StepConst &c, bool test, void *stream) {
   const size_t shm = (size_t)(64 + 2 * c.E) * (16 + 2 * c.E) * sizeof(double);
+  const size_t shm_col = shm + (size_t)(c.E + 1) * (c.E + 1) * sizeof(double);
+  if (shm_col <= 160 * 1024) {  // the column kernel with J in LDS (eps <= 48)
+    if (test)
+      hipLaunchKernelGGL((k_weighted_col<true>), dim3(rl.nwork), dim3(256), shm_col, (hipStream_t)stream, rl, c);
+    else
+      hipLaunchKernelGGL((k_weighted_col<false>), dim3(rl.nwork), dim3(256), shm_col, (hipStream_t)stream, rl, c);
+    return check_launch();
+  }
   if (test)
     hipLaunchKernelGGL((k_weighted<true>), dim3(rl.nwork), dim3(256), shm, (hipStream_t)stream, rl, c);
   else
