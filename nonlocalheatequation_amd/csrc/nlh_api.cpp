@@ -194,7 +194,7 @@ struct nlh_solver {
   int kernel = NLH_KERNEL_EXACT;
   int fast_r = 2;  // columns per lane of the fast kernel (NLH_FAST_R=1|2|4: 64/128/256-column strips)
   bool pair = false;  // two steps per pass (nlh_pair.h); production fast mode (NLH_PAIR=0 disables)
-  bool wide = false;  // k_wide (nlh_wide.h) for eps 17..32
+  bool wide = false;  // k_wide (nlh_wide.h) for eps 17..48
   bool weighted = false;  // k_weighted: non-constant influence function
   double *d_wt = nullptr, *d_qj = nullptr;  // J tables (influence != 0)
   int halo = 0;       // halo rows/columns held per block: eps, or 2*eps with pair
@@ -366,10 +366,12 @@ int build_rectlists(nlh_solver *s, int kind) {
       }
       seg_h = own ? s->p.seg_rows : (int)best;
     } else if (s->wide) {
-      // k_wide: one-wave workgroups at two waves per SIMD (8 per CU, 214
-      // VGPRs at E = 32; profiles/r02/wide_bench_*), one round
+      // k_wide: one-wave workgroups, all resident in one round: two waves per
+      // SIMD up to E = 40 (8 per CU, 214 VGPRs at E = 32;
+      // profiles/r02/wide_bench_*), one beyond (4 per CU)
+      const int per_cu = std::max(1, std::min(8, nlh::wide_blocks_per_cu(E)));
       seg_h = own ? s->p.seg_rows
-                  : (int)std::max<int64_t>(2 * E, ceil_div(strip_rows, (int64_t)8 * s->cus));
+                  : (int)std::max<int64_t>(2 * E, ceil_div(strip_rows, (int64_t)per_cu * s->cus));
     } else {
       seg_h = own ? s->p.seg_rows
                   : (int)std::max<int64_t>(nlh::fast_seg_min(E), ceil_div(strip_rows, 1024));

@@ -95,9 +95,10 @@ int fast_strip_width(int E, int want_r);  // 64*R columns per strip
 int fast_seg_min(int E);                  // smallest sensible segment height
 // Work-item counts are filled into rl by the caller (wg_begin/nwork).
 int launch_fast(const RectList &rl, const StepConst &c, bool test, int want_r, void *stream);
-// large horizons (nlh_wide.h, eps in [17, 32]): single-step, 64-column strips,
+// large horizons (nlh_wide.h, eps in [17, 48]): single-step, 64-column strips,
 // centre fold (needs kc), production and fast test mode
 bool wide_supported(int E);
+int wide_blocks_per_cu(int E);  // resident k_wide workgroups per CU
 int launch_wide(const RectList &rl, const StepConst &c, bool test, void *stream);
 // two-step pass (nlh_pair.h): production mode, eps in [1, 16]
 bool pair_supported(int E);

@@ -507,7 +507,8 @@ static int check_launch() {
 // Fast-kernel variants, instantiated in nlh_fast_e*.hip (parallel build):
 //   E = 1..16        128-column strips (R = 2); E <= 8 also 256-column (R = 4)
 //                    and 64-column (R = 1)
-// E = 17..32 run k_wide (nlh_wide.h); larger horizons run k_exact.
+// E = 17..48 run k_wide (nlh_wide.h); larger horizons run k_weighted (J = 1,
+// to eps 52) or k_exact.
 #define NLH_FAST_EXTERN(E, R)                                                            \
   extern template int launch_fast_er<E, R, true>(const RectList &, const StepConst &, hipStream_t); \
   extern template int launch_fast_er<E, R, false>(const RectList &, const StepConst &, hipStream_t);
@@ -522,16 +523,37 @@ NLH_FAST_EXTERN(5, 1) NLH_FAST_EXTERN(6, 1) NLH_FAST_EXTERN(7, 1) NLH_FAST_EXTER
 NLH_FAST_EXTERN(9, 1) NLH_FAST_EXTERN(10, 1) NLH_FAST_EXTERN(11, 1) NLH_FAST_EXTERN(12, 1)
 NLH_FAST_EXTERN(13, 1) NLH_FAST_EXTERN(14, 1) NLH_FAST_EXTERN(15, 1) NLH_FAST_EXTERN(16, 1)
 
-// Large horizons (nlh_wide.h), instantiated in nlh_wide_e*.hip for E = 17..32
+// Large horizons (nlh_wide.h), instantiated in nlh_wide_e*.hip for E = 17..48
 #define NLH_WIDE_EXTERN(E)                                                             \
   extern template int launch_wide_e<E, true>(const RectList &, const StepConst &, hipStream_t); \
-  extern template int launch_wide_e<E, false>(const RectList &, const StepConst &, hipStream_t);
+  extern template int launch_wide_e<E, false>(const RectList &, const StepConst &, hipStream_t); \
+  extern template int wide_blocks_per_cu_e<E>();
 NLH_WIDE_EXTERN(17) NLH_WIDE_EXTERN(18) NLH_WIDE_EXTERN(19) NLH_WIDE_EXTERN(20)
 NLH_WIDE_EXTERN(21) NLH_WIDE_EXTERN(22) NLH_WIDE_EXTERN(23) NLH_WIDE_EXTERN(24)
 NLH_WIDE_EXTERN(25) NLH_WIDE_EXTERN(26) NLH_WIDE_EXTERN(27) NLH_WIDE_EXTERN(28)
 NLH_WIDE_EXTERN(29) NLH_WIDE_EXTERN(30) NLH_WIDE_EXTERN(31) NLH_WIDE_EXTERN(32)
+NLH_WIDE_EXTERN(33) NLH_WIDE_EXTERN(34) NLH_WIDE_EXTERN(35) NLH_WIDE_EXTERN(36)
+NLH_WIDE_EXTERN(37) NLH_WIDE_EXTERN(38) NLH_WIDE_EXTERN(39) NLH_WIDE_EXTERN(40)
+NLH_WIDE_EXTERN(41) NLH_WIDE_EXTERN(42) NLH_WIDE_EXTERN(43) NLH_WIDE_EXTERN(44)
+NLH_WIDE_EXTERN(45) NLH_WIDE_EXTERN(46) NLH_WIDE_EXTERN(47) NLH_WIDE_EXTERN(48)
 
-bool wide_supported(int E) { return E >= 17 && E <= 32; }
+bool wide_supported(int E) { return E >= 17 && E <= 48; }
+
+#define NLH_WIDE_CASES(X)                                                                          \
+  X(17) X(18) X(19) X(20) X(21) X(22) X(23) X(24) X(25) X(26) X(27) X(28) X(29) X(30) X(31) X(32) \
+  X(33) X(34) X(35) X(36) X(37) X(38) X(39) X(40) X(41) X(42) X(43) X(44) X(45) X(46) X(47) X(48)
+
+int wide_blocks_per_cu(int E) {
+  switch (E) {
+#define NLH_CASEWO(EE) \
+  case EE:             \
+    return wide_blocks_per_cu_e<EE>();
+    NLH_WIDE_CASES(NLH_CASEWO)
+#undef NLH_CASEWO
+    default:
+      return 0;
+  }
+}
 
 int launch_wide(const RectList &rl, const StepConst &c, bool test, void *stream) {
   hipStream_t st = (hipStream_t)stream;
@@ -539,9 +561,7 @@ int launch_wide(const RectList &rl, const StepConst &c, bool test, void *stream)
 #define NLH_CASEW(EE) \
   case EE:            \
     return test ? launch_wide_e<EE, true>(rl, c, st) : launch_wide_e<EE, false>(rl, c, st);
-    NLH_CASEW(17) NLH_CASEW(18) NLH_CASEW(19) NLH_CASEW(20) NLH_CASEW(21) NLH_CASEW(22)
-    NLH_CASEW(23) NLH_CASEW(24) NLH_CASEW(25) NLH_CASEW(26) NLH_CASEW(27) NLH_CASEW(28)
-    NLH_CASEW(29) NLH_CASEW(30) NLH_CASEW(31) NLH_CASEW(32)
+    NLH_WIDE_CASES(NLH_CASEW)
 #undef NLH_CASEW
     default:
       return -1;
@@ -638,7 +658,7 @@ int launch_pair(const RectList &rl, const StepConst &c, int variant, void *strea
   }
 }
 
-bool fast_supported(int E) { return E >= 1 && E <= 32; }
+bool fast_supported(int E) { return E >= 1 && E <= 48; }
 
 int fast_lanes_cols(int E, int want_r) {
   if (E > 16 || want_r == 1) return 1;

@@ -1,5 +1,5 @@
 // nlh_wide.h -- single-step production kernel for large horizons, k_wide
-// (E = 17..32; C4's eps = 32 among them).  Same operator as k_fast (reference
+// (E = 17..48; C4's eps = 32 among them).  Same operator as k_fast (reference
 // sum_local, src/2d_nonlocal_serial.cpp:256-270, J = 1; update :279-284), laid
 // out for one wave per SIMD:
 //
@@ -332,11 +332,26 @@ __global__ __launch_bounds__(64, 1) void k_wide(RectList L, StepConst C) {
   wait_vmcnt<0>();  // drain the clamped tail DMAs and the stores
 }
 
+// rows per chunk: 12 up to E = 32; 8 beyond, where the 2E + CH accumulators
+// fill the 256 arch VGPRs (E = 40: 256, E = 48: 274 with AGPRs, no scratch;
+// one wave per SIMD past E = 40)
+template <int E>
+constexpr int wide_chunk() { return E <= 32 ? kWideC : 8; }
+
 template <int E, bool TEST>
 int launch_wide_e(const RectList &rl, const StepConst &c, hipStream_t st) {
-  hipLaunchKernelGGL((k_wide<E, kWideC, TEST>), dim3(rl.nwork), dim3(64), 0, st, rl, c);
+  hipLaunchKernelGGL((k_wide<E, wide_chunk<E>(), TEST>), dim3(rl.nwork), dim3(64), 0, st, rl, c);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : (int)e;
+}
+
+// resident k_wide workgroups (one wave each) per CU, for the host's choice of
+// segment height
+template <int E>
+int wide_blocks_per_cu_e() {
+  int n = 0;
+  const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_wide<E, wide_chunk<E>(), false>, 64, 0);
+  return e == hipSuccess ? n : 0;
 }
 
 }  // namespace nlh

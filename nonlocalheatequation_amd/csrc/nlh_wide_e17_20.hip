@@ -12,4 +12,8 @@ template int launch_wide_e<19, true>(const RectList &, const StepConst &, hipStr
 template int launch_wide_e<19, false>(const RectList &, const StepConst &, hipStream_t);
 template int launch_wide_e<20, true>(const RectList &, const StepConst &, hipStream_t);
 template int launch_wide_e<20, false>(const RectList &, const StepConst &, hipStream_t);
+template int wide_blocks_per_cu_e<17>();
+template int wide_blocks_per_cu_e<18>();
+template int wide_blocks_per_cu_e<19>();
+template int wide_blocks_per_cu_e<20>();
 }  // namespace nlh

@@ -12,4 +12,8 @@ template int launch_wide_e<23, true>(const RectList &, const StepConst &, hipStr
 template int launch_wide_e<23, false>(const RectList &, const StepConst &, hipStream_t);
 template int launch_wide_e<24, true>(const RectList &, const StepConst &, hipStream_t);
 template int launch_wide_e<24, false>(const RectList &, const StepConst &, hipStream_t);
+template int wide_blocks_per_cu_e<21>();
+template int wide_blocks_per_cu_e<22>();
+template int wide_blocks_per_cu_e<23>();
+template int wide_blocks_per_cu_e<24>();
 }  // namespace nlh

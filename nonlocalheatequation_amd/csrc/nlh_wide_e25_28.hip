@@ -12,4 +12,8 @@ template int launch_wide_e<27, true>(const RectList &, const StepConst &, hipStr
 template int launch_wide_e<27, false>(const RectList &, const StepConst &, hipStream_t);
 template int launch_wide_e<28, true>(const RectList &, const StepConst &, hipStream_t);
 template int launch_wide_e<28, false>(const RectList &, const StepConst &, hipStream_t);
+template int wide_blocks_per_cu_e<25>();
+template int wide_blocks_per_cu_e<26>();
+template int wide_blocks_per_cu_e<27>();
+template int wide_blocks_per_cu_e<28>();
 }  // namespace nlh

@@ -12,4 +12,8 @@ template int launch_wide_e<31, true>(const RectList &, const StepConst &, hipStr
 template int launch_wide_e<31, false>(const RectList &, const StepConst &, hipStream_t);
 template int launch_wide_e<32, true>(const RectList &, const StepConst &, hipStream_t);
 template int launch_wide_e<32, false>(const RectList &, const StepConst &, hipStream_t);
+template int wide_blocks_per_cu_e<29>();
+template int wide_blocks_per_cu_e<30>();
+template int wide_blocks_per_cu_e<31>();
+template int wide_blocks_per_cu_e<32>();
 }  // namespace nlh

@@ -145,10 +145,10 @@ def _disk_bound(eps, nt, dh, dt, k, c_factor, scale, test):
     return nt * N.disk_count(E) * 2.0 ** -53 * S * 2 * (scale + (1.0 if test else 0.0))
 
 
-@pytest.mark.parametrize("eps", [33, 40, 52])
+@pytest.mark.parametrize("eps", [49, 52])
 @pytest.mark.parametrize("test", [False, True])
 def test_large_eps_weighted_j1(oracle, eps, test):
-    """eps 33..52 (beyond the nested-window kernels): AUTO/FAST run k_weighted
+    """eps 49..52 (beyond the nested-window kernels): AUTO/FAST run k_weighted
     with J = 1 over an LDS tile; per node within 1e-12 of field scale or the
     disk sum's rounding bound, L2 as the oracle's; EXACT stays bitwise."""
     nx, ny, nt = 150, 133, 3
@@ -209,6 +209,30 @@ def test_wide_kernel_vs_oracle(oracle, eps, test):
     assert np.max(np.abs(u - u_ref)) <= 1e-12 * scale
     if test:
         assert abs(l2 - l2_ref) <= 1e-10 * l2_ref
+
+
+@pytest.mark.parametrize("eps", [33, 37, 40, 44, 48])
+@pytest.mark.parametrize("test", [False, True])
+def test_wide_kernel_large_eps(oracle, eps, test):
+    """k_wide past eps 32 (8-row accumulator chunks, up to 2E + 8 = 104 live
+    accumulators: AGPRs past E = 40, one wave per SIMD): per node within
+    1e-12 of field scale (or the disk sum's rounding bound), L2 as the
+    oracle's, on a lattice narrower than two strips and shorter than 3 eps."""
+    nx, ny, nt = 150, 133, 3
+    dh = 1.0 / nx
+    r = N.BatchRow(nx, ny, nt, eps, 1.0, 0.5 * eps ** 4 * dh * dh / (8 * N.disk_count(eps)), dh)
+    u0 = None if test else np.random.default_rng(eps).uniform(-1, 1, size=(ny, nx))
+    p = oracle.params(nx, ny, eps, r.k, r.dt, dh, int(test))
+    ref = oracle.run(p, nt, u0)
+    u, (l2, _), info = _gpu_run_j(r, test, "auto", "constant", u0)
+    assert info.pass_kernel == "k_wide" and info.kernel == N.KERNEL_FAST
+    d = np.max(np.abs(u - ref))
+    scale = np.max(np.abs(ref))
+    assert d <= max(1e-12 * scale, _disk_bound(eps, nt, dh, r.dt, r.k, 8, scale, test)), d
+    if test:
+        l2_ref = oracle.errors(p, nt, ref)[0]
+        n = nx * ny
+        assert abs(l2 - l2_ref) <= 1e-10 * l2_ref + d * (2 * np.sqrt(n * l2_ref) + n * d)
 
 
 @pytest.mark.parametrize("seg", [1, 9, 64, 1000])
