@@ -70,9 +70,42 @@ __device__ __forceinline__ double tree_sum(const double (&p)[N]) {
     return tree_sum<LO, (LO + HI) / 2>(p) + tree_sum<(LO + HI) / 2 + 1, HI>(p);
 }
 
+// Inclusive prefix sum of x over the 64 lanes of the wave: Hillis-Steele
+// within each 16-lane row (DPP row_shr 1, 2, 4, 8, zero-filled at the row
+// start), then the row totals carried by row_bcast:15 / row_bcast:31.  fp64 as
+// two 32-bit DPP moves per step.
+__device__ __forceinline__ double wave_prefix_sum(double x) {
+  auto sh = [](double v, auto ctrl, auto rmask, auto bc) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), decltype(ctrl)::value,
+                                               decltype(rmask)::value, 0xf, decltype(bc)::value);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), decltype(ctrl)::value,
+                                               decltype(rmask)::value, 0xf, decltype(bc)::value);
+    return __hiloint2double(hi, lo);
+  };
+  using I = std::integral_constant<int, 0>;
+  (void)sizeof(I);
+  x += sh(x, std::integral_constant<int, 0x111>{}, std::integral_constant<int, 0xf>{}, std::true_type{});
+  x += sh(x, std::integral_constant<int, 0x112>{}, std::integral_constant<int, 0xf>{}, std::true_type{});
+  x += sh(x, std::integral_constant<int, 0x114>{}, std::integral_constant<int, 0xf>{}, std::true_type{});
+  x += sh(x, std::integral_constant<int, 0x118>{}, std::integral_constant<int, 0xf>{}, std::true_type{});
+  x += sh(x, std::integral_constant<int, 0x142>{}, std::integral_constant<int, 0xa>{}, std::false_type{});
+  x += sh(x, std::integral_constant<int, 0x143>{}, std::integral_constant<int, 0xc>{}, std::false_type{});
+  return x;
+}
+
 // ABL (diagnostics, timing only): 1 = a scheduling barrier between rows
+// PS: row windows from a prefix sum of the staged row instead of the nested
+// pair sums.  The lane's 16-byte chunk of the staged row (two, past 128
+// doubles: E > 32) is summed, scanned over the wave (DPP; the second chunk
+// adds the first scan's total) and written back as P(k) = staged[0] + .. +
+// staged[k]; a used level L is then
+// H_L = P(c+L) - P(c-L-1): two LDS reads and one subtraction per USED level
+// (19 of 32 at E = 32, 24 of 40 at E = 40) instead of two reads and two adds
+// per level.  The difference of two prefix sums of at most 160 values rounds at ~2^-45 of the
+// row's magnitude: far inside the 1e-12 field-scale tolerance once alpha ~ 1/N
+// scales the disk sum.
 template <int E, int CH, bool TEST, int D = kWideD, int ABL = 0, int PIN = 1, bool AB = false, int OBP = 16,
-          bool SPLIT8 = true>
+          bool SPLIT8 = true, bool PS = false>
 __global__ __launch_bounds__(64, 1) void k_wide(RectList L, StepConst C) {
   constexpr int W = 64;                 // output columns per strip
   constexpr int EP = (E + 1) & ~1;      // staged halo columns per side (16-B rows)
@@ -92,11 +125,17 @@ __global__ __launch_bounds__(64, 1) void k_wide(RectList L, StepConst C) {
   static_assert(D * G + CH < 64, "vmcnt range");
   static_assert(CH % PIN == 0, "rows per pin");
 
-  __shared__ __attribute__((aligned(16))) double ring[K * RWS + (TEST ? K * W + 2 * K : 0)];
+  static_assert(!PS || (RW <= 256 && !AB), "prefix-sum rows: at most four staged doubles per lane");
+  constexpr int NP = PS ? RW + 2 : 0;  // prefix row: pfx[1] = 0, pfx[2 + k] = P(k)
+  __shared__ __attribute__((aligned(16))) double ring[K * RWS + (TEST ? K * W + 2 * K : 0) + NP];
   double *lwr = ring + K * RWS;  // L_h[W0] rows (TEST), same slots as the u rows
   double *syr = lwr + K * W;     // sin(2 pi y dh) pairs (TEST), same slots
+  double *pfx = ring + K * RWS + (TEST ? K * W + 2 * K : 0);  // PS: prefix row
 
   const int lane = (int)threadIdx.x;
+  if constexpr (PS) {
+    if (lane == 0) pfx[1] = 0.0;  // P(-1); the row writes start at pfx[2]
+  }
   const int work = xcd_remap(blockIdx.x, gridDim.x);
   const int ri = find_rect(L, work);
   const Rect &Rc = L.r[ri];
@@ -244,6 +283,43 @@ __global__ __launch_bounds__(64, 1) void k_wide(RectList L, StepConst C) {
         }
       };
       const double wc = AB ? ((E % 2 == 0) ? wpair(E / 2).x : wpair(E / 2).y) : wrow[E];
+      if constexpr (PS) {
+        // prefix row of the staged row (slot i), then the used levels' windows
+        const double *srow = ring + (i & (K - 1)) * RWS;
+        double2 ab = make_double2(0.0, 0.0);
+        if (2 * lane < RW) ab = *reinterpret_cast<const double2 *>(srow + 2 * lane);
+        double2 cd = make_double2(0.0, 0.0);  // second chunk of the lane (E > 32)
+        if constexpr (RW > 128)
+          if (2 * (lane + 64) < RW) cd = *reinterpret_cast<const double2 *>(srow + 2 * (lane + 64));
+        const double sv = wave_prefix_sum(ab.x + ab.y);
+        double sw = 0.0;
+        if constexpr (RW > 128) {
+          const double tot = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(sv), 63),
+                                              __builtin_amdgcn_readlane(__double2loint(sv), 63));
+          sw = wave_prefix_sum(cd.x + cd.y) + tot;
+        }
+        asm volatile("" ::: "memory");
+        if (2 * lane < RW) *reinterpret_cast<double2 *>(pfx + 2 + 2 * lane) = make_double2(sv - ab.y, sv);
+        if constexpr (RW > 128)
+          if (2 * (lane + 64) < RW)
+            *reinterpret_cast<double2 *>(pfx + 2 + 2 * (lane + 64)) = make_double2(sw - cd.y, sw);
+        asm volatile("" ::: "memory");  // in order per wave: the reads below see every lane's write
+        acc[c + 2 * E] = wc;
+        acc[c] += wc;
+        const double *pl = pfx + 2 + EP + lane;  // P(centre column + k) at pl[k]
+        auto plevel = [&](auto lc) __attribute__((always_inline)) {
+          constexpr int Lv = decltype(lc)::value + 1;
+          if constexpr (wide_taps(E, Lv) > 0) {
+            const double h = pl[Lv] - pl[-Lv - 1];
+            auto tap = [&](auto kk) __attribute__((always_inline)) {
+              constexpr int dy = wide_tap_dy(E, Lv, decltype(kk)::value);
+              acc[c + E - dy] += h;
+            };
+            static_for<wide_taps(E, Lv)>(tap);
+          }
+        };
+        static_for<E>(plevel);
+      } else {
       load_group(std::integral_constant<int, 0>{});
       // dy = -E: first term of output a = c + 2E; dy = +E: last of a = c
       acc[c + 2 * E] = wc;
@@ -299,6 +375,7 @@ __global__ __launch_bounds__(64, 1) void k_wide(RectList L, StepConst C) {
         }
       };
       static_for<NG>(group);
+      }
       acc[c + E] = fma(kc, wc, acc[c + E]);
       if constexpr (TEST) {
         // b = -(2 pi st) W0 - ct L_h[W0] at output k = i - E
@@ -338,9 +415,17 @@ __global__ __launch_bounds__(64, 1) void k_wide(RectList L, StepConst C) {
 template <int E>
 constexpr int wide_chunk() { return E <= 32 ? kWideC : 8; }
 
+// prefix-sum row windows where the staged row is one 16-byte chunk per lane
+// (E <= 32): C4 at 8192^2 143 vs 128 G node/s.  Past 32 the two-chunk scan
+// lifts k_wide over 256 VGPRs (one wave per SIMD): eps 40 71 vs 102 G, eps 48
+// 54 vs 66 G (profiles/r02/evidence/wide_ps/), so those keep the nested sums
+template <int E>
+constexpr bool wide_ps() { return 64 + 2 * ((E + 1) & ~1) <= 128; }
+
 template <int E, bool TEST>
 int launch_wide_e(const RectList &rl, const StepConst &c, hipStream_t st) {
-  hipLaunchKernelGGL((k_wide<E, wide_chunk<E>(), TEST>), dim3(rl.nwork), dim3(64), 0, st, rl, c);
+  hipLaunchKernelGGL((k_wide<E, wide_chunk<E>(), TEST, kWideD, 0, 1, false, 16, true, wide_ps<E>()>),
+                     dim3(rl.nwork), dim3(64), 0, st, rl, c);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : (int)e;
 }
@@ -350,7 +435,8 @@ int launch_wide_e(const RectList &rl, const StepConst &c, hipStream_t st) {
 template <int E>
 int wide_blocks_per_cu_e() {
   int n = 0;
-  const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_wide<E, wide_chunk<E>(), false>, 64, 0);
+  const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+      &n, k_wide<E, wide_chunk<E>(), false, kWideD, 0, 1, false, 16, true, wide_ps<E>()>, 64, 0);
   return e == hipSuccess ? n : 0;
 }
 

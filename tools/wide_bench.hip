@@ -75,8 +75,9 @@ int main(int argc, char **argv) {
   const int cus = prop.multiProcessorCount;
   std::vector<Variant> vs = {
       {"wide_C12_D6", k_wide<E, 12, false, 6>, 64, 8},
-      {"wide_C12_D4", k_wide<E, 12, false, 4>, 64, 8},
-      {"wide_C16_D6", k_wide<E, 16, false, 6>, 64, 8},
+      {"wide_ps_C12_D6", k_wide<E, 12, false, 6, 0, 1, false, 16, true, true>, 64, 8},
+      {"wide_ps_C8_D6", k_wide<E, 8, false, 6, 0, 1, false, 16, true, true>, 64, 8},
+      {"wide_ps_C16_D6", k_wide<E, 16, false, 6, 0, 1, false, 16, true, true>, 64, 8},
   };
   std::vector<double> ref((size_t)n * n), got((size_t)n * n);
   hipEvent_t e0, e1;
