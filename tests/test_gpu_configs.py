@@ -7,6 +7,8 @@ and long-run parity.
   production two-step pass, checked per node against the bit-parity kernel
   k_exact on one block (bitwise equal to the reference's per-term order on
   every oracle-sized case), plus the bitwise linearity step(2u) = 2 step(u).
+* C4 (8192^2, eps=32) in its 1x1, 2x2 and 2x4 layouts (RCCL to self): the
+  large-horizon kernel k_wide vs k_exact per node, and linearity.
 * C5 uneven (tests/load_balance_25s_8n.txt: 5 x 5 tiles of 9216^2 over 8
   owners, 1-7 tiles each, 2.1 G nodes = 16384^2 per GPU on average): the
   owners' blocks on one device (NLH_VIRTUAL_RANKS=8), pieces between owners
@@ -92,6 +94,32 @@ def test_c3_blocks_over_rccl_self(monkeypatch):
     u0 *= 2.0
     monkeypatch.setenv("NLH_RCCL_SELF", "1")
     u2, _ = _run(n, n, eps, nt, "fast", u0, tiles=(2, 4), split=True)
+    assert _bitwise_double(uf, u2)
+
+
+@pytest.mark.parametrize("tiles", [(1, 1), (2, 2), (2, 4)])
+def test_c4_full_size_wide_kernel(monkeypatch, tiles):
+    """C4 (8192^2, eps=32, N=3209) at full size in its 1-, 4- and 8-GPU block
+    layouts (blocks exchanging eps-wide halos over RCCL to self): k_wide with
+    prefix-sum row windows, two steps, per node vs k_exact (the reference's
+    per-term order), plus the bitwise linearity step(2u) = 2 step(u)."""
+    n, eps, nt = 8192, 32, 2
+    rng = np.random.default_rng(32)
+    u0 = rng.uniform(-1.0, 1.0, size=(n, n))
+    split = tiles != (1, 1)
+    if split:
+        monkeypatch.setenv("NLH_RCCL_SELF", "1")
+    uf, info = _run(n, n, eps, nt, "fast", u0, tiles=tiles, split=split)
+    assert info.pass_kernel == "k_wide" and info.nblocks == tiles[0] * tiles[1]
+    monkeypatch.delenv("NLH_RCCL_SELF", raising=False)
+    ue, info_e = _run(n, n, eps, nt, "exact", u0)
+    assert info_e.kernel == N.KERNEL_EXACT
+    d, scale = _max_abs_diff(uf, ue)
+    assert d <= 1e-12 * scale, f"max |diff| {d} vs scale {scale}"
+    del ue
+    if split:
+        monkeypatch.setenv("NLH_RCCL_SELF", "1")
+    u2, _ = _run(n, n, eps, nt, "fast", 2.0 * u0, tiles=tiles, split=split)
     assert _bitwise_double(uf, u2)
 
 
