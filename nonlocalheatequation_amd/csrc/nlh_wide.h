@@ -415,12 +415,13 @@ __global__ __launch_bounds__(64, 1) void k_wide(RectList L, StepConst C) {
 template <int E>
 constexpr int wide_chunk() { return E <= 32 ? kWideC : 8; }
 
-// prefix-sum row windows where the staged row is one 16-byte chunk per lane
-// (E <= 32): C4 at 8192^2 143 vs 128 G node/s.  Past 32 the two-chunk scan
-// lifts k_wide over 256 VGPRs (one wave per SIMD): eps 40 71 vs 102 G, eps 48
-// 54 vs 66 G (profiles/r02/evidence/wide_ps/), so those keep the nested sums
+// prefix-sum row windows where they keep k_wide within the 256 VGPRs of two
+// waves per SIMD (hipcc 7.2, 8-row chunks past 32: 240 / 248 / 256 at E = 33 /
+// 34 / 35, 260+ from 36): C4 at 8192^2 143 vs 128 G node/s, eps 33 113 vs
+// 108 G.  Past that the two-chunk scan costs the second wave: eps 40 71 vs
+// 102 G, eps 48 54 vs 66 G (profiles/r02/evidence/wide_ps/) -- nested sums
 template <int E>
-constexpr bool wide_ps() { return 64 + 2 * ((E + 1) & ~1) <= 128; }
+constexpr bool wide_ps() { return E <= 35; }
 
 template <int E, bool TEST>
 int launch_wide_e(const RectList &rl, const StepConst &c, hipStream_t st) {
