@@ -18,6 +18,12 @@ INC     := -Iinclude -I$(CSRC)
 HIPFLAGS := --offload-arch=$(ARCH) -O3 $(CXXSTD) -fPIC $(WARN) $(INC) -munsafe-fp-atomics
 HOSTFLAGS := -O2 $(CXXSTD) -fPIC $(WARN) $(INC) -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include
 
+# build identity: hash of every library source, the public header and this
+# Makefile (flags), in sorted path order -- nonlocalheatequation_amd.source_build_id()
+# recomputes it from the tree; tests, smoke() and bench.py compare the two
+BUILD_ID_SRCS := $(sort $(wildcard $(CSRC)/*.hip $(CSRC)/*.h $(CSRC)/*.cpp) include/nlh.h Makefile)
+BUILD_ID := $(shell cat $(BUILD_ID_SRCS) | sha256sum | cut -c1-16)
+
 FAST_UNITS := $(sort $(wildcard $(CSRC)/nlh_fast_e*.hip $(CSRC)/nlh_pair_e*.hip $(CSRC)/nlh_wide_e*.hip))
 FAST_OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(FAST_UNITS))
 LIB_OBJS := $(OBJDIR)/nlh_kernels.o $(FAST_OBJS) $(OBJDIR)/nlh_api.o $(OBJDIR)/nlh_plan.o $(OBJDIR)/nlh_1d.o
@@ -25,7 +31,7 @@ LIB_OBJS := $(OBJDIR)/nlh_kernels.o $(FAST_OBJS) $(OBJDIR)/nlh_api.o $(OBJDIR)/n
 # size cap so every accumulator stays in registers (no scratch)
 UNROLL  := -mllvm -pragma-unroll-threshold=1000000
 DRIVERS  := $(BINDIR)/2d_nonlocal_serial $(BINDIR)/2d_nonlocal_async $(BINDIR)/2d_nonlocal_distributed \
-            $(BINDIR)/1d_nonlocal_serial $(BINDIR)/2d_domain_decomposition
+            $(BINDIR)/1d_nonlocal_serial $(BINDIR)/2d_domain_decomposition $(BINDIR)/comm_id_check
 DRV_COMMON := $(OBJDIR)/driver_common.o $(OBJDIR)/vtu_writer.o
 
 all: lib drivers oracle
@@ -52,8 +58,8 @@ $(OBJDIR)/nlh_pair_%.o: $(CSRC)/nlh_pair_%.hip $(CHDRS) $(CSRC)/nlh_pair.h | $(O
 $(OBJDIR)/nlh_wide_%.o: $(CSRC)/nlh_wide_%.hip $(CHDRS) $(CSRC)/nlh_wide.h | $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) $(UNROLL) -c $< -o $@
 
-$(OBJDIR)/nlh_api.o: $(CSRC)/nlh_api.cpp $(CSRC)/nlh_device.h $(CSRC)/nlh_plan.h include/nlh.h | $(OBJDIR)
-	$(HIPCC) $(HOSTFLAGS) -x c++ -c $< -o $@
+$(OBJDIR)/nlh_api.o: $(CSRC)/nlh_api.cpp $(BUILD_ID_SRCS) | $(OBJDIR)
+	$(HIPCC) $(HOSTFLAGS) -DNLH_BUILD_ID='"$(BUILD_ID)"' -x c++ -c $< -o $@
 
 $(OBJDIR)/nlh_1d.o: $(CSRC)/nlh_1d.cpp include/nlh.h | $(OBJDIR)
 	$(HIPCC) $(HOSTFLAGS) -x c++ -c $< -o $@
@@ -72,6 +78,11 @@ $(OBJDIR)/vtu_writer.o: $(CSRC)/drivers/vtu_writer.cpp $(CSRC)/drivers/vtu_write
 
 $(BINDIR)/%: $(CSRC)/drivers/%.cpp $(DRV_COMMON) $(LIBDIR)/libnlh.so | $(BINDIR)
 	g++ -O2 $(CXXSTD) $(WARN) $(INC) $< $(DRV_COMMON) -o $@ -L$(LIBDIR) -lnlh \
+	    -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)' -Wl,-rpath,$(ROCM)/lib -lpthread
+
+# test harness of the drivers' TCP id bootstrap (tests/test_drivers.py, CPU)
+$(BINDIR)/comm_id_check: tools/comm_id_check.cpp $(DRV_COMMON) $(LIBDIR)/libnlh.so | $(BINDIR)
+	g++ -O2 $(CXXSTD) $(WARN) $(INC) -I$(CSRC)/drivers $< $(DRV_COMMON) -o $@ -L$(LIBDIR) -lnlh \
 	    -Wl,-rpath,'$$ORIGIN/../$(LIBDIR)' -Wl,-rpath,$(ROCM)/lib -lpthread
 
 clean:

@@ -18,10 +18,17 @@ ghost strips exchanged over RCCL.  ``--strong --lattice 32768`` fixes the
 total lattice (C3: 2x4 blocks of 16384 x 8192 on 8 GPUs).
 
 Prints one JSON line (rank 0) with the roofline of the dominant kernel
-(HIP events on the stencil's own stream), its physical limits from the
-committed rocprofv3 PMC profile of the same kernel and workload, and a
-bounded CPU baseline (the oracle's tiled 2d_nonlocal_async restatement on
-the host cores this job may use).
+(HIP events on the stencil's own stream), its physical limits from rocprofv3
+PMC counters of the same kernel and workload -- collected live by this run
+(--pmc auto: three counter passes over tools/prof_step.py as child
+processes, before this process touches the GPU), else a committed record
+carrying the same library build id -- and a bounded CPU baseline (the
+oracle's tiled 2d_nonlocal_async restatement on the host cores this job may
+use).
+
+Warm-up: W steps, continued (untimed) until at least --warmup-ms of stepping
+has passed, so the timed region starts at the clocks a sustained run holds;
+the line reports both W and the warm-up steps actually run.
 """
 from __future__ import annotations
 
@@ -111,19 +118,89 @@ def workload_name(nb, eps, strong, test, nx, ny) -> str:
     return f"{nb}x{nb} lattice per GPU, eps={eps}, {mode}"
 
 
-def read_pmc(kernel_name: str, wkey: str):
+def read_pmc(kernel_name: str, wkey: str, build_id: str):
     """The committed rocprofv3 PMC summary of this kernel on this workload
     (tools/pmc_summary.py: FETCH_SIZE doubled per the gfx950 correction +
-    WRITE_SIZE, SQ_INSTS_VALU; separate passes), if one exists."""
+    WRITE_SIZE, SQ_INSTS_VALU; separate passes), if one exists AND was
+    profiled on a library with this build id."""
     path = os.path.join(ROOT, "profiles", "pmc", f"{kernel_name}__{wkey}.json")
     try:
         with open(path) as f:
             d = json.load(f)
     except (OSError, ValueError):
         return None, path
-    if d.get("kernel_match") != kernel_name or d.get("workload") != wkey:
+    if d.get("kernel_match") != kernel_name or d.get("workload") != wkey or d.get("build_id") != build_id:
         return None, path
     return d, path
+
+
+# one counter group per rocprofv3 pass (MI355X_MICROARCH.md: FETCH_SIZE and
+# WRITE_SIZE cannot share a pass; <= 8 SQ counters per pass)
+PMC_PASSES = ["FETCH_SIZE", "WRITE_SIZE",
+              "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU"]
+
+
+def live_pmc(args, wkey: str):
+    """rocprofv3 --pmc passes over tools/prof_step.py running this bench's
+    workload, each a child process under its own time limit.  Called before
+    this process loads libnlh or touches the GPU.  Returns the record
+    read_pmc would return (same keys; kernel, node-updates per launch and
+    build id as the profiled program reported them), or None when rocprofv3
+    is unavailable or a pass fails."""
+    import csv
+    import shutil
+    import statistics
+    import tempfile
+    prof = shutil.which("rocprofv3")
+    if not prof:
+        return None
+    env = dict(os.environ, NLH_N=str(args.lattice), NLH_EPS=str(args.eps), NLH_TEST=str(int(args.test_mode)),
+               NLH_KERNEL=args.kernel, NLH_INFLUENCE=args.influence, NLH_SEG=str(args.seg_rows),
+               TMPDIR="/tmp")
+    vals, durs, seen = {}, [], set()
+    with tempfile.TemporaryDirectory(dir="/tmp") as td:
+        for i, grp in enumerate(PMC_PASSES):
+            out = os.path.join(td, f"p{i}")
+            cmd = ["timeout", "-s", "KILL", "120", prof, "--pmc", *grp.split(), "--kernel-trace",
+                   "--output-format", "csv", "-d", out, "-o", "run", "--",
+                   sys.executable, os.path.join(ROOT, "tools", "prof_step.py")]
+            try:
+                r = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True,
+                                   timeout=150)
+            except (OSError, subprocess.SubprocessError):
+                return None
+            ok = [l.split() for l in r.stdout.splitlines() if l.startswith("ok ")]
+            if r.returncode != 0 or not ok or len(ok[-1]) != 5:
+                return None
+            seen.add(tuple(ok[-1][1:]))
+            kernel_name, spp, nodes, build_id = ok[-1][1], int(ok[-1][2]), int(ok[-1][3]), ok[-1][4]
+            key = kernel_name + "<"
+            for root, _, files in os.walk(out):
+                for fn in files:
+                    path = os.path.join(root, fn)
+                    if fn.endswith("counter_collection.csv"):
+                        for row in csv.DictReader(open(path)):
+                            if key in row["Kernel_Name"]:
+                                vals.setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
+                    elif fn.endswith("kernel_trace.csv"):
+                        for row in csv.DictReader(open(path)):
+                            if key in row["Kernel_Name"]:
+                                durs.append(int(row["End_Timestamp"]) - int(row["Start_Timestamp"]))
+    med = {k: statistics.median(v) for k, v in vals.items()}
+    if len(seen) != 1 or not {"FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU"} <= set(med):
+        return None
+    node_updates = nodes * spp
+    rd, wr = 2.0 * med["FETCH_SIZE"] * 1024, med["WRITE_SIZE"] * 1024  # gfx950 FETCH_SIZE half-count
+    rec = {"kernel_match": kernel_name, "workload": wkey, "build_id": build_id, "source": "live",
+           "median": med, "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
+           "hbm_bytes_per_launch": rd + wr, "valu_insts_per_launch": med["SQ_INSTS_VALU"],
+           "node_updates_per_launch": node_updates,
+           "profiled_duration_us_median": statistics.median(durs) / 1e3 if durs else None,
+           "correction": "FETCH_SIZE x2 (gfx950 half-count of wide streaming reads), KiB -> bytes"}
+    if med.get("SQ_WAVE_CYCLES"):
+        rec["share_of_wave_cycles"] = {k: med[k] / med["SQ_WAVE_CYCLES"] for k in ("SQ_WAIT_ANY", "SQ_ACTIVE_INST_VALU")
+                                       if k in med}
+    return rec
 
 
 def free_port() -> int:
@@ -173,6 +250,10 @@ def main() -> int:
     ap.add_argument("--kernel", default="fast", choices=["fast", "exact", "auto"])
     ap.add_argument("--seg-rows", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--warmup-ms", type=float, default=300.0,
+                    help="continue the untimed warm-up until this much stepping has passed")
+    ap.add_argument("--pmc", default="auto", choices=["auto", "off"],
+                    help="auto: collect the roofline's PMC counters live (N=1, rocprofv3 on PATH)")
     # secondary workloads (the default line is C2): --eps 32 --lattice 8192 is
     # C4; --lattice 32768 --strong is C3 (total lattice fixed as N grows);
     # --test-mode times the manufactured-solution step and reports its L2
@@ -188,7 +269,17 @@ def main() -> int:
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         return spawn_ranks(args.gpus)
 
+    wkey = workload_key(nb, eps, args.strong, args.test_mode) + ("_linear" if args.influence == "linear" else "")
+    pmc_live = None
+    if args.pmc == "auto" and args.gpus == 1 and "WORLD_SIZE" not in os.environ:
+        pmc_live = live_pmc(args, wkey)  # child processes; this one has not loaded libnlh yet
+
     import nonlocalheatequation_amd as N
+    build_id = N.build_id()
+    if build_id != N.source_build_id():
+        print(f"libnlh build {build_id} does not match the sources ({N.source_build_id()}): make lib",
+              file=sys.stderr)
+        return 4
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -240,8 +331,25 @@ def main() -> int:
             print(f"ranks own {owned} nodes of {nx * ny}", file=sys.stderr)
             return 3
     s.test_init()
+    # warm-up: W steps, then more until --warmup-ms of stepping has passed (the
+    # clocks a sustained run holds); every rank runs the same count (rank 0's)
     s.run(args.warmup)
     s.synchronize()
+    warm = args.warmup
+    tw = time.perf_counter()
+    chunk = max(2, args.warmup)
+    while warm < 100000:
+        go = (time.perf_counter() - tw) * 1e3 < args.warmup_ms
+        if dist is not None:  # rank 0 decides, so every rank runs the same passes (the exchange is collective)
+            import torch
+            g = torch.tensor([int(go)], dtype=torch.int64)
+            dist.broadcast(g, src=0)
+            go = bool(g.item())
+        if not go:
+            break
+        s.run(chunk)
+        s.synchronize()
+        warm += chunk
 
     def barrier():
         s.synchronize()
@@ -287,8 +395,12 @@ def main() -> int:
     achieved_gbs = alg_bytes / avg_launch_s / 1e9
     fp64_equiv_tflops = 2.0 * info.disk_points * nu_launch / avg_launch_s / 1e12
 
-    wkey = workload_key(nb, eps, args.strong, args.test_mode) + ("_linear" if args.influence == "linear" else "")
-    pmc, pmc_path = read_pmc(kname, wkey) if nranks == 1 else (None, None)
+    pmc, pmc_path = None, None
+    if pmc_live and pmc_live["kernel_match"] == kname and pmc_live["build_id"] == build_id \
+            and pmc_live["node_updates_per_launch"] == nu_launch:
+        pmc, pmc_path = pmc_live, "live"
+    elif nranks == 1:
+        pmc, pmc_path = read_pmc(kname, wkey, build_id)
     traffic = pmc["hbm_bytes_per_launch"] if pmc else None
     physical = None
     if pmc:
@@ -311,8 +423,9 @@ def main() -> int:
             "kernel_rate_gnu": rate_launch,
             "frac_of_ceiling": rate_launch / min(hbm_ceiling, valu_ceiling),
             "wait_share_of_wave_cycles": pmc.get("share_of_wave_cycles", {}).get("SQ_WAIT_ANY"),
-            "source": os.path.relpath(pmc_path, ROOT),
-            "profiled_commit": pmc.get("commit"),
+            "source": "live rocprofv3 --pmc passes of this run (tools/prof_step.py, same workload)"
+                      if pmc_path == "live" else os.path.relpath(pmc_path, ROOT),
+            "build_id": pmc.get("build_id"),
         }
 
     result = None
@@ -329,6 +442,8 @@ def main() -> int:
             "nranks_seen": len(owned),
             "steps": args.steps,
             "warmup": args.warmup,
+            "warmup_steps_run": warm,
+            "build_id": build_id,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
             "scaling": "strong" if args.strong else "weak",

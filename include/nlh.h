@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define NLH_ABI_VERSION 6
+#define NLH_ABI_VERSION 7
 
 enum nlh_status {
   NLH_OK = 0,
@@ -157,8 +157,8 @@ typedef struct nlh_info {
   int32_t steps_per_pass;  /* 2: production fast mode fuses two steps per
                               pass over HBM (one halo exchange per pass)   */
   char    pass_kernel[32]; /* device kernel of one full pass: "k_pair_split",
-                              "k_pair_mw", "k_pair", "k_pair_pf", "k_fast",
-                              "k_wide", "k_weighted", "k_exact_lds" or "k_exact" */
+                              "k_fast", "k_wide", "k_weighted", "k_exact_lds"
+                              or "k_exact"                                 */
   int32_t owners;          /* owner ids in the tile map: nranks, or the
                               NLH_VIRTUAL_RANKS count (nlh_rebalance sizes) */
   int32_t reserved_;
@@ -173,8 +173,11 @@ int nlh_get_info(const nlh_solver *s, nlh_info *info);
  * launch group on the stream that runs it (interior and edge bands), so
  * halo waits are not counted -- the GPU counterpart of the reference's busy
  * rate, 10000 - idle-rate (src/2d_nonlocal_distributed.cpp:112-128,855-860).
- * nlh_kernel_time returns the summed duration and the number of time steps
- * advanced since the last enable.                                          */
+ * The interior and band groups of a pass run concurrently on two streams and
+ * both count, so busy time exceeds wall time where they overlap.  With
+ * NLH_VIRTUAL_RANKS each virtual rank's launches are separate, each with its
+ * own event pair.  nlh_kernel_time returns the summed duration and the
+ * number of time steps advanced since the last enable.                     */
 int nlh_kernel_timing(nlh_solver *s, int enable);
 int nlh_kernel_time(nlh_solver *s, double *total_ms, int64_t *steps);
 
@@ -216,8 +219,8 @@ int nlh_repartition(nlh_solver *s, const int32_t *owner);
  * after step t when t % nbalance == 0, :1306-1309).  busy time per rank is
  * this rank's stencil time since busy timing was enabled (nlh_kernel_timing
  * (s, 2)), all-gathered over RCCL, or busy_in[nranks] when non-NULL (with
- * NLH_VIRTUAL_RANKS one GPU runs every owner: the measured time is
- * apportioned by owned tiles, nranks = the virtual count).  apply != 0:
+ * NLH_VIRTUAL_RANKS each virtual rank's own measured stencil time, nranks =
+ * the virtual count).  apply != 0:
  * nlh_balance_owner picks the map and nlh_repartition applies it, and busy
  * timing restarts.  owner_out (tiles_x*tiles_y) and busy_out (nranks), both
  * optional, receive the resulting map and the busy times used.  Returns the
@@ -234,6 +237,23 @@ int nlh_rebalance(nlh_solver *s, const double *busy_in, int32_t apply, int32_t *
  * (a global rectangle copied from the owner's interior into the halo of
  * block dst_block of dst_rank).                                           */
 int64_t nlh_halo_plan(const nlh_params *p, int64_t *pieces, int64_t cap);
+
+/* Host-only exchange layout, for tests of the decomposition: the halo pieces
+ * rank p->rank packs for (dir 0) or unpacks from (dir 1) other ranks per
+ * pass, in the order nlh_create lays them into the per-peer RCCL messages.
+ * Returns the count and, if `out` is non-NULL, up to `cap` records of 8
+ * int64 each:  {peer, dir, offset, gx0, gy0, w, h, piece}
+ * (offset: doubles into the message to / from `peer`; piece: index into the
+ * plan nlh_halo_plan lists per destination).  What rank A sends to B must
+ * match, piece for piece and offset for offset, what B expects from A.    */
+int64_t nlh_exchange_plan(const nlh_params *p, int64_t *out, int64_t cap);
+
+/* Build identity: a hash of libnlh's kernel and host sources, this header and
+ * the Makefile (compile flags), fixed when the library is built
+ * (nonlocalheatequation_amd.source_build_id() recomputes it from a source
+ * tree).  The tests, smoke() and bench.py check the library they load
+ * against the checked-out sources.                                        */
+const char *nlh_build_id(void);
 
 /* Host-only block plan: number of device blocks over ALL ranks and, if
  * `blocks` is non-NULL, up to `cap` records of 6 int64 each:

@@ -22,6 +22,8 @@ Reference correspondences::
 from __future__ import annotations
 
 import ctypes
+import glob
+import hashlib
 import os
 from dataclasses import dataclass
 
@@ -31,7 +33,7 @@ __all__ = [
     "KERNEL_AUTO", "KERNEL_EXACT", "KERNEL_FAST", "INFLUENCE_CONSTANT", "INFLUENCE_LINEAR", "NLHError", "Solver",
     "lib", "lib_path", "comm_unique_id", "resolve_owner", "halo_plan", "block_plan",
     "disk_count", "batch_tester", "BatchRow", "Solver1D", "batch_tester_1d", "balance_owner",
-    "partition_tiles",
+    "partition_tiles", "exchange_plan", "build_id", "source_build_id",
 ]
 
 KERNEL_AUTO, KERNEL_EXACT, KERNEL_FAST = 0, 1, 2
@@ -41,6 +43,7 @@ INFLUENCE_CONSTANT, INFLUENCE_LINEAR = 0, 1
 _INFLUENCE_NAMES = {"constant": INFLUENCE_CONSTANT, "linear": INFLUENCE_LINEAR}
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
+_ROOT = os.path.dirname(_HERE)
 
 
 def lib_path() -> str:
@@ -111,6 +114,9 @@ _SIGNATURES = {
                       ctypes.c_int64),
     "nlh_block_plan": ([ctypes.POINTER(_Params), ctypes.POINTER(ctypes.c_int64), ctypes.c_int64],
                        ctypes.c_int64),
+    "nlh_exchange_plan": ([ctypes.POINTER(_Params), ctypes.POINTER(ctypes.c_int64), ctypes.c_int64],
+                          ctypes.c_int64),
+    "nlh_build_id": ([], ctypes.c_char_p),
     "nlh_balance_owner": ([ctypes.c_int64, ctypes.c_int64, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32),
                            ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
     "nlh_partition_tiles": ([ctypes.c_int64, ctypes.c_int64, ctypes.c_int32, ctypes.POINTER(ctypes.c_double),
@@ -145,6 +151,27 @@ def lib() -> ctypes.CDLL:
             fn.restype = res
         _lib = L
     return _lib
+
+
+def build_id() -> str:
+    """Build identity of the loaded libnlh (hash of its sources and flags)."""
+    return lib().nlh_build_id().decode()
+
+
+def source_build_id(root: str = _ROOT) -> str:
+    """The build identity a library built from the tree at `root` carries:
+    sha256 over the library sources, include/nlh.h and the Makefile in sorted
+    path order, first 16 hex digits (Makefile BUILD_ID)."""
+    csrc = os.path.join("nonlocalheatequation_amd", "csrc")
+    rel = []
+    for pat in ("*.hip", "*.h", "*.cpp"):
+        rel += [os.path.relpath(f, root) for f in glob.glob(os.path.join(root, csrc, pat))]
+    rel += [os.path.join("include", "nlh.h"), "Makefile"]
+    h = hashlib.sha256()
+    for r in sorted(rel):
+        with open(os.path.join(root, r), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
 
 
 def _check(rc: int, what: str) -> None:
@@ -230,6 +257,23 @@ def halo_plan(nx, ny, eps, tiles=(1, 1), owner=None, rank=0, nranks=1, split_til
     out = np.zeros((max(n, 0), 8), dtype=np.int64)
     if n > 0:
         lib().nlh_halo_plan(ctypes.byref(p), out.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), n)
+    del keep
+    return out
+
+
+def exchange_plan(nx, ny, eps, tiles=(1, 1), owner=None, rank=0, nranks=1, split_tiles=False, *,
+                  k=1.0, dt=1.0, dh=1.0, test=False, kernel="auto") -> np.ndarray:
+    """Host-only exchange layout of `rank`: (n, 8) int64 rows
+    {peer, dir (0 send, 1 receive), offset, gx0, gy0, w, h, piece} in the
+    order nlh_create packs / unpacks its per-peer RCCL messages."""
+    p, keep = _make_params(nx, ny, eps, k, dt, dh, test, kernel, -1, rank, nranks, 0,
+                           tiles, owner, None, split_tiles)
+    n = lib().nlh_exchange_plan(ctypes.byref(p), None, 0)
+    if n < 0:
+        _check(int(-n), "nlh_exchange_plan")
+    out = np.zeros((max(n, 0), 8), dtype=np.int64)
+    if n > 0:
+        lib().nlh_exchange_plan(ctypes.byref(p), out.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), n)
     del keep
     return out
 

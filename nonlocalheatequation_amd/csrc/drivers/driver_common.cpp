@@ -187,12 +187,17 @@ static bool recv_all(int fd, void *p, size_t n) {
   return true;
 }
 
-bool share_comm_id(const RankEnv &re, uint8_t id[NLH_COMM_ID_BYTES], std::string &err) {
+bool share_comm_id(const RankEnv &re, uint8_t id[NLH_COMM_ID_BYTES], std::string &err, bool fresh) {
   const char *addr = std::getenv("MASTER_ADDR");
   const int port = env_int("MASTER_PORT", 29517) + 1;  // next to torch's own store port
   if (!addr) addr = "127.0.0.1";
+  // every call is one bootstrap round (a batch row); a client names the
+  // round it wants, and rank 0 serves only clients of its current round, so a
+  // fast rank already at row r+1 cannot take row r's id
+  static uint32_t round = 0;
+  const uint32_t my_round = round++;
   if (re.rank == 0) {
-    if (nlh_comm_unique_id(id) != NLH_OK) {
+    if (fresh && nlh_comm_unique_id(id) != NLH_OK) {
       err = nlh_last_error();
       return false;
     }
@@ -208,13 +213,16 @@ bool share_comm_id(const RankEnv &re, uint8_t id[NLH_COMM_ID_BYTES], std::string
       ::close(lfd);
       return false;
     }
-    for (int i = 1; i < re.nranks; ++i) {
+    for (int served = 1; served < re.nranks;) {
       const int fd = ::accept(lfd, nullptr, nullptr);
-      if (fd < 0 || !send_all(fd, id, NLH_COMM_ID_BYTES)) {
-        err = "bootstrap accept/send failed";
+      if (fd < 0) {
+        err = "bootstrap accept failed";
         ::close(lfd);
         return false;
       }
+      uint32_t want = 0;
+      // a client of another round is turned away (it retries)
+      if (recv_all(fd, &want, sizeof(want)) && want == my_round && send_all(fd, id, NLH_COMM_ID_BYTES)) ++served;
       ::close(fd);
     }
     ::close(lfd);
@@ -228,11 +236,12 @@ bool share_comm_id(const RankEnv &re, uint8_t id[NLH_COMM_ID_BYTES], std::string
     return false;
   }
   bool ok = false;
-  for (int attempt = 0; attempt < 600 && !ok; ++attempt) {  // up to ~60 s
+  for (int attempt = 0; attempt < 1200 && !ok; ++attempt) {  // up to ~60 s
     const int fd = ::socket(AF_INET, SOCK_STREAM, 0);
-    if (::connect(fd, res->ai_addr, res->ai_addrlen) == 0) ok = recv_all(fd, id, NLH_COMM_ID_BYTES);
+    if (::connect(fd, res->ai_addr, res->ai_addrlen) == 0)
+      ok = send_all(fd, &my_round, sizeof(my_round)) && recv_all(fd, id, NLH_COMM_ID_BYTES);
     ::close(fd);
-    if (!ok) std::this_thread::sleep_for(std::chrono::milliseconds(100));
+    if (!ok) std::this_thread::sleep_for(std::chrono::milliseconds(50));
   }
   ::freeaddrinfo(res);
   if (!ok) err = "bootstrap: could not fetch the RCCL id from rank 0";

@@ -59,8 +59,10 @@ struct RankEnv {
   int rank = 0, nranks = 1, local_rank = 0;
 };
 RankEnv rank_env();
-// rank 0 generates the RCCL id and serves it to the others over TCP
-bool share_comm_id(const RankEnv &re, uint8_t id[NLH_COMM_ID_BYTES], std::string &err);
+// RCCL unique id from rank 0 to every rank over TCP (MASTER_ADDR,
+// MASTER_PORT + 1); fresh == false: rank 0 sends the id it was given instead
+// of a new RCCL id (tools/comm_id_check.cpp tests the bootstrap without a GPU)
+bool share_comm_id(const RankEnv &re, uint8_t id[NLH_COMM_ID_BYTES], std::string &err, bool fresh = true);
 
 int kernel_from_name(const std::string &s);
 // --influence constant|linear -> enum nlh_influence (-1 if unknown)

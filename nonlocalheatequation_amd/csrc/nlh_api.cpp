@@ -78,7 +78,6 @@ struct Resolved {
   bool wide = false;  // large-horizon single-step kernel (nlh_wide.h)
   bool weighted = false;  // non-constant J: k_weighted (fast) instead of the J = 1 kernels
   int halo = 0;       // eps, or 2*eps with pair
-  int ablate = 0;     // diagnostics only (NLH_ABLATE)
 };
 
 int resolve_config(const nlh_params &p, Resolved &r) {
@@ -124,19 +123,72 @@ int resolve_config(const nlh_params &p, Resolved &r) {
   }
   r.kernel = kern;
   r.wide = kern == NLH_KERNEL_FAST && nlh::wide_supported(E);
-  r.ablate = 0;
-  if (const char *ab = std::getenv("NLH_ABLATE")) r.ablate = std::atoi(ab);
   // fast mode advances two steps per pass (test mode too: the manufactured
   // source of both steps folded into the pass); a zero alpha (no centre fold)
   // keeps the single-step kernels
-  r.pair = kern == NLH_KERNEL_FAST && nlh::pair_supported(E) && fold_ok && r.ablate == 0;
+  r.pair = kern == NLH_KERNEL_FAST && nlh::pair_supported(E) && fold_ok;
   if (const char *pe = std::getenv("NLH_PAIR")) r.pair = r.pair && std::atoi(pe) != 0;
   r.halo = r.pair ? 2 * E : E;
   return NLH_OK;
 }
 
-// NLH_VIRTUAL_RANKS=V (diagnostics, one rank): resolve the owner map over V
-// virtual owners; every block stays on this GPU
+// Environment knobs libnlh reads (tuning and one-GPU verification).  Each one
+// changes only the schedule -- strip width, ring depth, segment sizing,
+// streams, the block decomposition over virtual ranks -- and the field stays
+// within the FAST tolerance of the run without it (bitwise for the EXACT
+// kernels): tests/test_gpu_parity.py::test_env_knobs_keep_results.  The
+// round-2 ablation switches (NLH_ABLATE, NLH_PAIR_ABLATE), which made the
+// library return meaningless fields, are gone; nlh_create refuses them, and
+// any knob value outside its range, instead of ignoring them.
+struct EnvKnob {
+  const char *name;
+  long lo, hi;
+};
+constexpr EnvKnob kEnvKnobs[] = {
+    {"NLH_PAIR", 0, 1},            // 0: single-step kernels instead of the two-step pass
+    {"NLH_FAST_R", 1, 4},          // k_fast columns per lane (1, 2 or 4)
+    {"NLH_FORCE_BANDS", 0, 1},     // exchange-path schedule on a single block
+    {"NLH_RCCL_SELF", 0, 1},       // one rank: halo pieces over RCCL to self
+    {"NLH_VIRTUAL_RANKS", 0, 1024},  // run V virtual ranks in this process
+    {"NLH_INT_PER_CU", 0, 64},     // interior workgroups per CU beside an exchange
+    {"NLH_SCHED", 0, 2},           // where the edge bands run
+    {"NLH_COMM_PRIO", 0, 1},       // exchange streams at the highest priority
+    {"NLH_PAIR_SPLIT", 1, 4},      // 4: production pass with 8-slot rings
+    {"NLH_PAIR_CU", 1, 16},        // pass workgroups per CU the segments are sized for
+    {"NLH_PAIR_TEST", 0, 1},       // 0: test-mode pass with 16-slot rings
+    {"NLH_PITCH_PAD", 0, 1024},    // extra doubles per padded row
+    {"NLH_BAND_SEG", 0, 1 << 20},  // edge-band segment height (0 = automatic)
+};
+constexpr const char *kRemovedKnobs[] = {"NLH_ABLATE", "NLH_PAIR_ABLATE"};
+
+int check_env() {
+  for (const char *name : kRemovedKnobs)
+    if (std::getenv(name))
+      return fail(NLH_ERR_ARG, std::string(name) +
+                                   " is set: ablation diagnostics are not part of libnlh (tools/pair_bench.hip)");
+  for (const EnvKnob &k : kEnvKnobs) {
+    const char *v = std::getenv(k.name);
+    if (!v || !*v) continue;
+    char *end = nullptr;
+    const long x = std::strtol(v, &end, 10);
+    if (*end != '\0' || x < k.lo || x > k.hi)
+      return fail(NLH_ERR_ARG, std::string(k.name) + "=" + v + ": expected an integer in [" + std::to_string(k.lo) +
+                                   ", " + std::to_string(k.hi) + "]");
+  }
+  if (const char *v = std::getenv("NLH_PAIR_SPLIT"))
+    if (*v && std::atoi(v) != 1 && std::atoi(v) != 4) return fail(NLH_ERR_ARG, "NLH_PAIR_SPLIT must be 1 or 4");
+  return NLH_OK;
+}
+
+// NLH_VIRTUAL_RANKS=V (one process, one GPU): the owner map is resolved over
+// V virtual ranks and this process runs all of them -- every virtual rank
+// keeps its own blocks, per-peer message buffers, pack/unpack lists and busy
+// time exactly as a real rank would (build_exchange with me = v); what a real
+// run sends from rank A to rank B travels from A's send buffer into B's
+// receive buffer through ncclSend/ncclRecv to self, grouped as a real run's
+// exchange.  Gather, error norms, repartition and rebalance take the same
+// per-rank paths.  RCCL refuses two ranks on one device, so this is how the
+// multi-rank code runs on a one-GPU box.
 int virtual_ranks(const nlh_params &p) {
   if (p.nranks != 1) return 0;
   const char *v = std::getenv("NLH_VIRTUAL_RANKS");
@@ -146,6 +198,7 @@ int virtual_ranks(const nlh_params &p) {
 
 struct LocalBlock {
   int plan_index = 0;
+  int owner = 0;  // (virtual) rank owning the block
   nlh::GRect r;
   int64_t pitch = 0, rows = 0;
   int32_t xl = 0;
@@ -177,7 +230,9 @@ struct Flag {
 constexpr size_t kEvFold = 4096;  // timing events kept before folding (nlh_run)
 
 struct Peer {
-  int rank = 0;
+  int me = 0;     // the (virtual) rank of this process holding the buffers
+  int rank = 0;   // the peer rank
+  int mate = -1;  // virtual ranks: index of the (rank, me) entry receiving what me sends
   int64_t send_count = 0, recv_count = 0;  // doubles
   double *send = nullptr, *recv = nullptr;
 };
@@ -198,9 +253,7 @@ struct nlh_solver {
   bool weighted = false;  // k_weighted: non-constant influence function
   double *d_wt = nullptr, *d_qj = nullptr;  // J tables (influence != 0)
   int halo = 0;       // halo rows/columns held per block: eps, or 2*eps with pair
-  int ablate = 0;     // diagnostics only (NLH_ABLATE), never set in production
-  int pair_ablate = 0;  // diagnostics only (NLH_PAIR_ABLATE)
-  int pair_split = 1;  // 1 k_pair_split (default), 0 k_pair, 2 k_pair_mw, 3 k_pair_pf (NLH_PAIR_SPLIT)
+  int pair_split = 1;  // production k_pair_split rings: 1 = D8/B4 (default), 6 = D4/B2 (NLH_PAIR_SPLIT=4)
   // test-mode pass: 5 = k_pair_split<TEST> with 8-slot rings (D=4, B=2; 322 vs
   // 287 G node/s at C2 for the production rings, profiles/r02/tune_test.jsonl),
   // 4 = D=8, B=4 (NLH_PAIR_TEST=0)
@@ -212,9 +265,8 @@ struct nlh_solver {
   bool force_bands = false;  // diagnostics (NLH_FORCE_BANDS): exchange-path schedule on one block
   bool rccl_self = false;    // diagnostics (NLH_RCCL_SELF): one rank, local pieces over RCCL to self
   bool exchange_planned = false;  // the plan has halo pieces (set before the rect lists)
-  // NLH_VIRTUAL_RANKS: per plan piece, 1 if it crosses virtual owners (goes
-  // over RCCL to self); empty otherwise
-  std::vector<uint8_t> vremote;
+  int vranks = 0;       // NLH_VIRTUAL_RANKS count (0: one real rank per process)
+  std::vector<int> mine;  // ranks this process runs: {rank}, or 0 .. vranks-1
   int owners = 1;  // owner ids in the tile map: nranks, or NLH_VIRTUAL_RANKS
   // exchange schedule (profiles/r01/sched): interior workgroups per CU in the
   // segment model when an exchange runs beside it (RCCL kernels need the LDS
@@ -248,10 +300,12 @@ struct nlh_solver {
   std::vector<hipEvent_t> ev_pool;
   size_t ev_used = 0;
   std::vector<int> ev_steps;  // time steps covered by each timed event pair
+  std::vector<int> ev_owner;  // busy timing: the (virtual) rank of each event pair
   // pairs already folded into a running total (long busy windows: the pool
   // is drained every kEvFold events instead of growing with the run)
   double ev_acc_ms = 0.0;
   int64_t ev_acc_steps = 0;
+  std::vector<double> ev_acc_owner;  // folded busy milliseconds per owner
   int64_t device_bytes = 0;
   char arch[32] = {0};
   // logging snapshots (nlh_snapshot_begin / _wait): owned nodes packed block
@@ -395,10 +449,13 @@ int build_rectlists(nlh_solver *s, int kind) {
     out.clear();
     int w = 0;
     for (auto &it : items) {
-      if (out.empty() || out.back().nrects >= nlh::kMaxRects) {
+      // a list never mixes (virtual) ranks: busy time is measured per rank
+      const int own = s->blocks[it.blk].owner;
+      if (out.empty() || out.back().nrects >= nlh::kMaxRects || out.back().owner != own) {
         if (!out.empty()) out.back().nwork = w;
         out.emplace_back();
         std::memset(&out.back(), 0, sizeof(nlh::RectList));
+        out.back().owner = own;
         w = 0;
       }
       nlh::RectList &rl = out.back();
@@ -455,75 +512,87 @@ double *node_ptr(const LocalBlock &b, int k, int64_t gx, int64_t gy) {
 }
 
 int build_exchange(nlh_solver *s) {
-  const int me = s->p.rank;
   std::map<int, size_t> local_of_plan;  // plan block index -> local index
   for (size_t i = 0; i < s->blocks.size(); ++i) local_of_plan[s->blocks[i].plan_index] = i;
-  // a piece travels over RCCL when its blocks sit on different ranks; with
-  // NLH_RCCL_SELF (diagnostics, one rank) every piece between two blocks of
-  // this rank goes through ncclSend/ncclRecv to self instead of a local copy,
-  // so the pack -> RCCL -> unpack path runs on a single GPU.  With
-  // NLH_VIRTUAL_RANKS (diagnostics) only pieces between blocks of different
-  // virtual owners do: the block structure and message pattern of a
-  // multi-rank run, every rank's blocks on this one GPU.
-  auto remote = [&](size_t pi) {
-    const nlh::Piece &pc = s->plan.pieces[pi];
-    if (!s->vremote.empty()) return s->vremote[pi] != 0;
-    return pc.src_rank != pc.dst_rank || s->rccl_self;
-  };
-  // peers and message sizes in plan order
-  std::map<int, Peer> peers;
-  for (size_t pi = 0; pi < s->plan.pieces.size(); ++pi) {
-    const nlh::Piece &pc = s->plan.pieces[pi];
-    if (!remote(pi)) continue;
-    if (pc.src_rank == me) peers[pc.dst_rank].send_count += pc.r.w * pc.r.h;
-    if (pc.dst_rank == me) peers[pc.src_rank].recv_count += pc.r.w * pc.r.h;
+  // a piece travels over RCCL when its blocks sit on different (virtual)
+  // ranks; with NLH_RCCL_SELF (one real rank) every piece goes through
+  // ncclSend/ncclRecv to self instead of a local copy
+  const bool self_all = s->rccl_self && s->vranks == 0;
+  std::vector<std::vector<nlh::XferEntry>> lay(s->mine.size());
+  std::map<std::pair<int, int>, Peer> peers;  // (me, peer rank)
+  for (size_t m = 0; m < s->mine.size(); ++m) {
+    const int me = s->mine[m];
+    lay[m] = nlh::exchange_layout(s->plan, me, self_all);
+    for (const auto &e : lay[m]) {
+      const nlh::Piece &pc = s->plan.pieces[e.piece];
+      Peer &pr = peers[{me, e.peer}];
+      pr.me = me;
+      pr.rank = e.peer;
+      int64_t &cnt = e.dir == 0 ? pr.send_count : pr.recv_count;
+      cnt = std::max(cnt, e.offset + pc.r.w * pc.r.h);
+    }
   }
   for (auto &kv : peers) {
     Peer &pr = kv.second;
-    pr.rank = kv.first;
     if (pr.send_count) HIP_TRY(hipMalloc(&pr.send, pr.send_count * sizeof(double)));
     if (pr.recv_count) HIP_TRY(hipMalloc(&pr.recv, pr.recv_count * sizeof(double)));
     s->device_bytes += (pr.send_count + pr.recv_count) * (int64_t)sizeof(double);
     s->halo_bytes += pr.send_count * (int64_t)sizeof(double);
+    s->peers.push_back(pr);  // ordered by (me, peer)
   }
+  if (s->vranks) {
+    // what virtual rank A sends to B lands in B's receive buffer from A: the
+    // two message layouts must agree (they do by construction: both walk the
+    // plan in order -- checked here before any transfer is enqueued)
+    for (size_t i = 0; i < s->peers.size(); ++i) {
+      Peer &pr = s->peers[i];
+      for (size_t j = 0; j < s->peers.size(); ++j)
+        if (s->peers[j].me == pr.rank && s->peers[j].rank == pr.me) pr.mate = (int)j;
+      const int64_t want = pr.mate >= 0 ? s->peers[pr.mate].recv_count : 0;
+      if (pr.send_count != want)
+        return fail(NLH_ERR_STATE, "internal: virtual rank " + std::to_string(pr.me) + " sends " +
+                                       std::to_string(pr.send_count) + " doubles to " + std::to_string(pr.rank) +
+                                       ", which expects " + std::to_string(want));
+    }
+  }
+  auto peer_of = [&](int me, int rank) -> Peer & {
+    for (auto &pr : s->peers)
+      if (pr.me == me && pr.rank == rank) return pr;
+    return s->peers.front();  // unreachable: every layout entry made a peer
+  };
   for (int k = 0; k < 2; ++k) {
-    std::map<int, int64_t> soff, roff;
     auto &pk = s->cl_pack[k], &up = s->cl_unpack[k], &lc = s->cl_local[k];
     pk.clear();
     up.clear();
     lc.clear();
-    for (size_t pi = 0; pi < s->plan.pieces.size(); ++pi) {
-      const nlh::Piece &pc = s->plan.pieces[pi];
-      const int64_t n = pc.r.w * pc.r.h;
-      int rc = NLH_OK;
-      if (!remote(pi)) {
-        if (pc.src_rank == me) {
+    for (size_t m = 0; m < s->mine.size(); ++m) {
+      for (const auto &e : lay[m]) {
+        const nlh::Piece &pc = s->plan.pieces[e.piece];
+        Peer &pr = peer_of(s->mine[m], e.peer);
+        int rc;
+        if (e.dir == 0) {
           const LocalBlock &sb = s->blocks[local_of_plan[pc.src_block]];
+          rc = add_copy(pk, node_ptr(sb, k, pc.r.x0, pc.r.y0), sb.pitch, pr.send + e.offset, pc.r.w, pc.r.w,
+                        pc.r.h);
+        } else {
           const LocalBlock &db = s->blocks[local_of_plan[pc.dst_block]];
-          rc = add_copy(lc, node_ptr(sb, k, pc.r.x0, pc.r.y0), sb.pitch,
-                        node_ptr(db, k, pc.r.x0, pc.r.y0), db.pitch, pc.r.w, pc.r.h);
+          rc = add_copy(up, pr.recv + e.offset, pc.r.w, node_ptr(db, k, pc.r.x0, pc.r.y0), db.pitch, pc.r.w,
+                        pc.r.h);
         }
         if (rc != NLH_OK) return rc;
-        continue;
       }
-      if (pc.src_rank == me) {
-        const LocalBlock &sb = s->blocks[local_of_plan[pc.src_block]];
-        Peer &pr = peers[pc.dst_rank];
-        rc = add_copy(pk, node_ptr(sb, k, pc.r.x0, pc.r.y0), sb.pitch,
-                      pr.send + soff[pc.dst_rank], pc.r.w, pc.r.w, pc.r.h);
-        soff[pc.dst_rank] += n;
-      }
-      if (rc == NLH_OK && pc.dst_rank == me) {
-        const LocalBlock &db = s->blocks[local_of_plan[pc.dst_block]];
-        Peer &pr = peers[pc.src_rank];
-        rc = add_copy(up, pr.recv + roff[pc.src_rank], pc.r.w,
-                      node_ptr(db, k, pc.r.x0, pc.r.y0), db.pitch, pc.r.w, pc.r.h);
-        roff[pc.src_rank] += n;
-      }
+    }
+    // pieces between blocks of one (virtual) rank: device copies
+    for (const auto &pc : s->plan.pieces) {
+      if (pc.src_rank != pc.dst_rank || self_all) continue;
+      if (!local_of_plan.count(pc.src_block)) continue;  // another process's blocks
+      const LocalBlock &sb = s->blocks[local_of_plan[pc.src_block]];
+      const LocalBlock &db = s->blocks[local_of_plan[pc.dst_block]];
+      const int rc = add_copy(lc, node_ptr(sb, k, pc.r.x0, pc.r.y0), sb.pitch, node_ptr(db, k, pc.r.x0, pc.r.y0),
+                              db.pitch, pc.r.w, pc.r.h);
       if (rc != NLH_OK) return rc;
     }
   }
-  for (auto &kv : peers) s->peers.push_back(kv.second);
   s->exchange = !s->plan.pieces.empty() || s->force_bands;
   return NLH_OK;
 }
@@ -537,17 +606,18 @@ hipEvent_t pool_event(nlh_solver *s) {
   return s->ev_pool[s->ev_used++];
 }
 
-int launch_stencil(nlh_solver *s, const std::vector<nlh::RectList> &v, hipStream_t st) {
+using RLIter = std::vector<nlh::RectList>::const_iterator;
+
+int launch_stencil(nlh_solver *s, RLIter b, RLIter e, hipStream_t st) {
   const bool test = s->p.test != 0;
-  for (const auto &rl : v) {
+  for (; b != e; ++b) {
+    const nlh::RectList &rl = *b;
     if (rl.nwork == 0) continue;
     int rc;
     if (s->weighted)
       rc = nlh::launch_weighted(rl, s->sc, test, st);
     else if (s->wide)
       rc = nlh::launch_wide(rl, s->sc, test, st);
-    else if (s->kernel == NLH_KERNEL_FAST && !test && s->ablate)
-      rc = nlh::launch_fast_ablation(rl, s->sc, s->ablate, st);
     else if (s->kernel == NLH_KERNEL_FAST)
       rc = nlh::launch_fast(rl, s->sc, test, s->fast_r, st);
     else
@@ -557,11 +627,11 @@ int launch_stencil(nlh_solver *s, const std::vector<nlh::RectList> &v, hipStream
   return NLH_OK;
 }
 
-int launch_pair_lists(nlh_solver *s, const std::vector<nlh::RectList> &v, hipStream_t st) {
-  for (const auto &rl : v) {
+int launch_pair_lists(nlh_solver *s, RLIter b, RLIter e, hipStream_t st) {
+  for (; b != e; ++b) {
+    const nlh::RectList &rl = *b;
     if (rl.nwork == 0) continue;
-    const int rc = s->pair_ablate ? nlh::launch_pair_ablation(rl, s->sc, s->pair_ablate, st)
-                                  : nlh::launch_pair(rl, s->sc, s->p.test ? s->pair_test : s->pair_split, st);
+    const int rc = nlh::launch_pair(rl, s->sc, s->p.test ? s->pair_test : s->pair_split, st);
     if (rc != 0) return fail(NLH_ERR_HIP, std::string("pair launch failed: ") + hipGetErrorString((hipError_t)rc));
   }
   return NLH_OK;
@@ -590,9 +660,20 @@ int enqueue_exchange(nlh_solver *s, int k) {
   if (launch_copy_lists(s->cl_pack[k], s->s_comm)) return NLH_ERR_HIP;
   if (!s->peers.empty()) {
     NCCL_TRY(ncclGroupStart());
-    for (auto &pr : s->peers) {
-      if (pr.send_count) NCCL_TRY(ncclSend(pr.send, pr.send_count, ncclDouble, pr.rank, s->comm, s->s_comm));
-      if (pr.recv_count) NCCL_TRY(ncclRecv(pr.recv, pr.recv_count, ncclDouble, pr.rank, s->comm, s->s_comm));
+    if (s->vranks) {
+      // every virtual A -> B message: A's send buffer for B into B's receive
+      // buffer from A, through RCCL to self (send/recv pairs match in issue
+      // order within the group)
+      for (auto &pr : s->peers) {
+        if (!pr.send_count) continue;
+        NCCL_TRY(ncclSend(pr.send, pr.send_count, ncclDouble, 0, s->comm, s->s_comm));
+        NCCL_TRY(ncclRecv(s->peers[pr.mate].recv, pr.send_count, ncclDouble, 0, s->comm, s->s_comm));
+      }
+    } else {
+      for (auto &pr : s->peers) {
+        if (pr.send_count) NCCL_TRY(ncclSend(pr.send, pr.send_count, ncclDouble, pr.rank, s->comm, s->s_comm));
+        if (pr.recv_count) NCCL_TRY(ncclRecv(pr.recv, pr.recv_count, ncclDouble, pr.rank, s->comm, s->s_comm));
+      }
     }
     NCCL_TRY(ncclGroupEnd());
   }
@@ -618,21 +699,32 @@ int enqueue_step(nlh_solver *s, int nsteps) {
   set_time(s, s->t);
   auto stencil = [&](const std::vector<nlh::RectList> &one, const std::vector<nlh::RectList> &pr,
                      hipStream_t st) {
-    bool any = false;
-    for (const auto &rl : two ? pr : one) any |= rl.nwork > 0;
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (s->timing == 2 && any) {  // busy time: this launch group only
-      e0 = pool_event(s);
-      e1 = pool_event(s);
-      if (!e0 || !e1) return fail(NLH_ERR_HIP, "event pool");
-      HIP_TRY(hipEventRecord(e0, st));
+    const std::vector<nlh::RectList> &v = two ? pr : one;
+    auto run = [&](RLIter b, RLIter e) {
+      return two ? launch_pair_lists(s, b, e, st) : launch_stencil(s, b, e, st);
+    };
+    if (s->timing != 2) return run(v.begin(), v.end());
+    // busy time: an event pair around each (virtual) rank's launches of this
+    // group (its lists are contiguous, build_rectlists); time steps are
+    // counted once, on the interior stream's first pair
+    bool first = true;
+    for (RLIter b = v.begin(); b != v.end();) {
+      RLIter e = b;
+      bool any = false;
+      while (e != v.end() && e->owner == b->owner) any |= (e++)->nwork > 0;
+      if (any) {
+        hipEvent_t e0 = pool_event(s), e1 = pool_event(s);
+        if (!e0 || !e1) return fail(NLH_ERR_HIP, "event pool");
+        HIP_TRY(hipEventRecord(e0, st));
+        if (const int r = run(b, e)) return r;
+        HIP_TRY(hipEventRecord(e1, st));
+        s->ev_steps.push_back(st == s->s_main && first ? nsteps : 0);
+        s->ev_owner.push_back(b->owner);
+        first = false;
+      }
+      b = e;
     }
-    const int r = two ? launch_pair_lists(s, pr, st) : launch_stencil(s, one, st);
-    if (e1) {
-      HIP_TRY(hipEventRecord(e1, st));
-      s->ev_steps.push_back(st == s->s_main ? nsteps : 0);  // steps counted on the interior group
-    }
-    return r;
+    return (int)NLH_OK;
   };
   int rc;
   if (!s->exchange) {
@@ -770,6 +862,7 @@ int create_impl(const nlh_params *pin, nlh_solver *s, ncclComm_t reuse_comm = nu
   const int64_t tx = p.tiles_x > 0 ? p.tiles_x : 1, ty = p.tiles_y > 0 ? p.tiles_y : 1;
   if (p.nx % tx || p.ny % ty) return fail(NLH_ERR_ARG, "tiles_x/tiles_y must divide nx/ny");
   if (p.kernel < NLH_KERNEL_AUTO || p.kernel > NLH_KERNEL_FAST) return fail(NLH_ERR_ARG, "bad kernel");
+  if (int rc = check_env()) return rc;
   s->p = p;
   s->p.tiles_x = tx;
   s->p.tiles_y = ty;
@@ -811,11 +904,9 @@ int create_impl(const nlh_params *pin, nlh_solver *s, ncclComm_t reuse_comm = nu
     s->fast_r = (v == 1 || v == 4) ? v : 2;
   }
   s->fast_r = nlh::fast_lanes_cols(E, s->fast_r);
-  s->ablate = rv.ablate;
   s->pair = rv.pair;
   s->wide = rv.wide;
   s->weighted = rv.weighted;
-  if (const char *pa = std::getenv("NLH_PAIR_ABLATE")) s->pair_ablate = std::atoi(pa);
   if (const char *fb = std::getenv("NLH_FORCE_BANDS")) s->force_bands = std::atoi(fb) != 0;
   if (const char *rs = std::getenv("NLH_RCCL_SELF")) s->rccl_self = p.nranks == 1 && std::atoi(rs) != 0;
   if (vranks) s->rccl_self = true;  // virtual owners talk over RCCL to self
@@ -824,25 +915,19 @@ int create_impl(const nlh_params *pin, nlh_solver *s, ncclComm_t reuse_comm = nu
   int prio_lo = 0, prio_hi = 0;  // NLH_COMM_PRIO=1: exchange + band streams at the highest priority
   if (const char *cp = std::getenv("NLH_COMM_PRIO"))
     if (std::atoi(cp) != 0) HIP_TRY(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
-  if (const char *ps = std::getenv("NLH_PAIR_SPLIT")) {
-    const int v = std::min(4, std::max(0, std::atoi(ps)));
-    s->pair_split = v == 4 ? 6 : v;  // 4: k_pair_split with 8-slot rings (variant 6)
-  }
+  if (const char *ps = std::getenv("NLH_PAIR_SPLIT"))
+    if (std::atoi(ps) == 4) s->pair_split = 6;  // k_pair_split with 8-slot rings (variant 6)
   if (const char *pc = std::getenv("NLH_PAIR_CU")) s->pair_cu = std::max(1, std::atoi(pc));
   if (const char *pt = std::getenv("NLH_PAIR_TEST")) s->pair_test = std::atoi(pt) == 0 ? 4 : 5;
-  if (s->pair_ablate >= 10000) s->pair_split = 1;
   s->halo = rv.halo;
   s->plan = nlh::make_plan(p.nx, p.ny, s->halo, tx, ty, s->owner, p.split_tiles == 0);
-  if (vranks) {
-    // blocks keep the virtual owners' shapes; all of them live on rank 0
-    s->vremote.resize(s->plan.pieces.size());
-    for (size_t i = 0; i < s->plan.pieces.size(); ++i) {
-      nlh::Piece &pc = s->plan.pieces[i];
-      s->vremote[i] = pc.src_rank != pc.dst_rank;
-      pc.src_rank = pc.dst_rank = 0;
-    }
-    for (auto &b : s->plan.blocks) b.rank = 0;
-  }
+  s->vranks = vranks;
+  s->mine.clear();
+  if (vranks)
+    for (int v = 0; v < vranks; ++v) s->mine.push_back(v);
+  else
+    s->mine.push_back((int)p.rank);
+  s->ev_acc_owner.assign(s->owners, 0.0);
 
   HIP_TRY(hipStreamCreateWithFlags(&s->s_main, hipStreamNonBlocking));
   HIP_TRY(hipStreamCreateWithPriority(&s->s_comm, hipStreamNonBlocking, prio_hi));
@@ -919,9 +1004,10 @@ int create_impl(const nlh_params *pin, nlh_solver *s, ncclComm_t reuse_comm = nu
   if (const char *pp = std::getenv("NLH_PITCH_PAD")) pitch_pad = 2 * (std::max(0, std::atoi(pp)) / 2);
   for (size_t i = 0; i < s->plan.blocks.size(); ++i) {
     const auto &bd = s->plan.blocks[i];
-    if (bd.rank != p.rank) continue;
+    if (!vranks && bd.rank != p.rank) continue;  // virtual ranks: this process runs every block
     LocalBlock b;
     b.plan_index = (int)i;
+    b.owner = bd.rank;
     b.r = bd.r;
     b.xl = (int32_t)XL;
     // whole 256-column strips stay in bounds; the pair kernel's last strip
@@ -1007,8 +1093,15 @@ double *tile_ptr(const nlh_solver *s, int local, int k, int64_t x0, int64_t y0) 
   return b.origin(k) + (y0 - b.r.y0) * b.pitch + (x0 - b.r.x0);
 }
 
+bool runs(const nlh_solver *s, int rank) {
+  return std::find(s->mine.begin(), s->mine.end(), rank) != s->mine.end();
+}
+
 // rebuild the solver for a new tile -> owner map, moving the tiles that
-// change rank over RCCL (src/2d_nonlocal_distributed.cpp:937-944)
+// change rank over RCCL (src/2d_nonlocal_distributed.cpp:937-944).  Per
+// (virtual) rank pair A -> B the moving tiles travel in tile order as one
+// message; with virtual ranks A's message goes through RCCL to self into B's
+// staging buffer, as a real run's would to rank B.
 int repartition_impl(nlh_solver *s, const std::vector<int32_t> &own) {
   if (s->snap_pending) return fail(NLH_ERR_STATE, "a snapshot is in flight (call nlh_snapshot_wait)");
   int rc = set_device(s);
@@ -1029,22 +1122,26 @@ int repartition_impl(nlh_solver *s, const std::vector<int32_t> &own) {
     g_err = keep;
     return rc;
   }
-  const int me = (int)p.rank;
   const int64_t tw = p.nx / p.tiles_x, th = p.ny / p.tiles_y;
   struct Mv {
     int64_t x0, y0;
     int src, dst;  // local block indices in s (source) and n (destination)
   };
   std::vector<Mv> local;
-  std::map<int, std::vector<Mv>> sends, recvs;  // by peer rank, tile order
+  // (sender, receiver) -> tiles in tile order; sends hold the sender's side,
+  // recvs the receiver's
+  std::map<std::pair<int, int>, std::vector<Mv>> sends, recvs;
   for (int64_t i = 0; i < p.tiles_x * p.tiles_y; ++i) {
     const int64_t x0 = (i % p.tiles_x) * tw, y0 = (i / p.tiles_x) * th;
     int ro, lo, rn, ln;
     locate(s, x0, y0, ro, lo);
     locate(n, x0, y0, rn, ln);
-    if (ro == me && rn == me) local.push_back({x0, y0, lo, ln});
-    else if (ro == me) sends[rn].push_back({x0, y0, lo, -1});
-    else if (rn == me) recvs[ro].push_back({x0, y0, -1, ln});
+    if (ro == rn && runs(s, ro)) {
+      local.push_back({x0, y0, lo, ln});
+      continue;
+    }
+    if (runs(s, ro)) sends[{ro, rn}].push_back({x0, y0, lo, -1});
+    if (runs(s, rn)) recvs[{ro, rn}].push_back({x0, y0, -1, ln});
   }
   const size_t tb = (size_t)(tw * th);
   const size_t pitch_b = (size_t)tw * sizeof(double);
@@ -1063,7 +1160,7 @@ int repartition_impl(nlh_solver *s, const std::vector<int32_t> &own) {
                          pitch_b, th, hipMemcpyDeviceToDevice, st) != hipSuccess)
       status = fail(NLH_ERR_HIP, "repartition local copy");
   }
-  std::map<int, double *> sbuf, rbuf;
+  std::map<std::pair<int, int>, double *> sbuf, rbuf;
   for (auto &kv : sends) {
     double *b = stage(kv.second.size());
     if (!b) { status = fail(NLH_ERR_HIP, "repartition staging"); break; }
@@ -1087,10 +1184,21 @@ int repartition_impl(nlh_solver *s, const std::vector<int32_t> &own) {
       status = fail(NLH_ERR_STATE, "internal: tiles change rank without a communicator");
     } else {
       bool ok = ncclGroupStart() == ncclSuccess;
-      for (auto &kv : sends)
-        ok = ok && ncclSend(sbuf[kv.first], kv.second.size() * tb, ncclDouble, kv.first, n->comm, st) == ncclSuccess;
-      for (auto &kv : recvs)
-        ok = ok && ncclRecv(rbuf[kv.first], kv.second.size() * tb, ncclDouble, kv.first, n->comm, st) == ncclSuccess;
+      if (s->vranks) {
+        for (auto &kv : sends) {  // A -> B: A's staged tiles into B's staging buffer, over RCCL to self
+          const size_t cnt = kv.second.size() * tb;
+          ok = ok && recvs.count(kv.first) && recvs[kv.first].size() == kv.second.size();
+          ok = ok && ncclSend(sbuf[kv.first], cnt, ncclDouble, 0, n->comm, st) == ncclSuccess;
+          ok = ok && ncclRecv(rbuf[kv.first], cnt, ncclDouble, 0, n->comm, st) == ncclSuccess;
+        }
+      } else {
+        for (auto &kv : sends)
+          ok = ok && ncclSend(sbuf[kv.first], kv.second.size() * tb, ncclDouble, kv.first.second, n->comm, st) ==
+                         ncclSuccess;
+        for (auto &kv : recvs)
+          ok = ok && ncclRecv(rbuf[kv.first], kv.second.size() * tb, ncclDouble, kv.first.first, n->comm, st) ==
+                         ncclSuccess;
+      }
       ok = (ncclGroupEnd() == ncclSuccess) && ok;
       if (!ok) status = fail(NLH_ERR_RCCL, "repartition send/recv");
     }
@@ -1133,17 +1241,22 @@ int fold_events(nlh_solver *s) {
     float ms = 0.f;
     HIP_TRY(hipEventElapsedTime(&ms, s->ev_pool[i], s->ev_pool[i + 1]));
     s->ev_acc_ms += ms;
+    const int own = s->ev_owner[i / 2];
+    if (own >= 0 && own < (int)s->ev_acc_owner.size()) s->ev_acc_owner[own] += ms;
   }
   for (int n : s->ev_steps) s->ev_acc_steps += n;
   s->ev_used = 0;
   s->ev_steps.clear();
+  s->ev_owner.clear();
   return NLH_OK;
 }
 
-// this rank's busy milliseconds since busy timing was enabled
-int local_busy(nlh_solver *s, double &ms) {
-  int64_t steps = 0;
-  return nlh_kernel_time(s, &ms, &steps);
+// busy milliseconds of each (virtual) rank this process runs since busy
+// timing was enabled (index = rank; ranks run elsewhere stay 0)
+int owner_busy(nlh_solver *s, std::vector<double> &ms) {
+  if (int rc = fold_events(s)) return rc;
+  ms = s->ev_acc_owner;
+  return NLH_OK;
 }
 
 }  // namespace
@@ -1156,6 +1269,9 @@ const char *nlh_last_error(void) { return g_err.c_str(); }
 
 int nlh_comm_unique_id(uint8_t id[NLH_COMM_ID_BYTES]) {
   if (!id) return fail(NLH_ERR_ARG, "null id");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+    return fail(NLH_ERR_HIP, "no HIP device visible (libnlh has no CPU fallback)");
   ncclUniqueId u;
   NCCL_TRY(ncclGetUniqueId(&u));
   std::memcpy(id, &u, sizeof(u));
@@ -1226,60 +1342,80 @@ int nlh_get_field(nlh_solver *s, double *u) {
 
 int nlh_gather_field(nlh_solver *s, int32_t root, double *u) {
   if (!s) return fail(NLH_ERR_ARG, "null solver");
-  if (root < 0 || root >= s->p.nranks) return fail(NLH_ERR_ARG, "bad root");
-  if (s->p.rank == root && !u) return fail(NLH_ERR_ARG, "root needs an output array");
+  if (root < 0 || root >= s->owners) return fail(NLH_ERR_ARG, "bad root");
+  const bool at_root = runs(s, root);
+  if (at_root && !u) return fail(NLH_ERR_ARG, "root needs an output array");
   int rc = set_device(s);
   if (rc) return rc;
-  if (s->p.rank == root) {
-    rc = nlh_get_field(s, u);
-    if (rc) return rc;
-  }
-  if (!s->comm) return NLH_OK;
+  HIP_TRY(hipStreamSynchronize(s->s_comm));
   HIP_TRY(hipStreamSynchronize(s->s_main));
-  // every non-root rank ships its blocks, packed in plan order
-  std::vector<int64_t> count(s->p.nranks, 0);
+  // the root's own blocks straight to the host
+  if (at_root)
+    for (auto &b : s->blocks)
+      if (b.owner == root)
+        HIP_TRY(hipMemcpy2D(u + b.r.y0 * s->p.nx + b.r.x0, s->p.nx * sizeof(double), b.origin(s->cur),
+                            b.pitch * sizeof(double), b.r.w * sizeof(double), b.r.h, hipMemcpyDeviceToHost));
+  if (!s->comm) return NLH_OK;
+  // every other (virtual) rank ships its blocks packed in plan order; the
+  // root unpacks by the plan.  With virtual ranks each one's message travels
+  // over RCCL to self, as a real rank's would to the root
+  std::vector<int64_t> count(s->owners, 0);
   for (auto &b : s->plan.blocks) count[b.rank] += b.r.w * b.r.h;
-  double *buf = nullptr;
   int64_t maxc = 1;
-  for (int r = 0; r < s->p.nranks; ++r) maxc = std::max(maxc, count[r]);
-  HIP_TRY(hipMalloc(&buf, maxc * sizeof(double)));
+  for (int r = 0; r < s->owners; ++r) maxc = std::max(maxc, count[r]);
+  double *sbuf = nullptr, *rbuf = nullptr;
+  HIP_TRY(hipMalloc(&sbuf, maxc * sizeof(double)));
+  if (hipMalloc(&rbuf, maxc * sizeof(double)) != hipSuccess) {
+    (void)hipFree(sbuf);
+    return fail(NLH_ERR_HIP, "gather buffer");
+  }
   int status = NLH_OK;
-  if (s->p.rank != root) {
+  auto pack = [&](int r) {
     int64_t off = 0;
     for (auto &b : s->blocks) {
-      if (hipMemcpy2DAsync(buf + off, b.r.w * sizeof(double), b.origin(s->cur), b.pitch * sizeof(double),
+      if (b.owner != r) continue;
+      if (hipMemcpy2DAsync(sbuf + off, b.r.w * sizeof(double), b.origin(s->cur), b.pitch * sizeof(double),
                            b.r.w * sizeof(double), b.r.h, hipMemcpyDeviceToDevice, s->s_comm) != hipSuccess)
         status = fail(NLH_ERR_HIP, "gather pack");
       off += b.r.w * b.r.h;
     }
-    if (status == NLH_OK && count[s->p.rank] &&
-        ncclSend(buf, count[s->p.rank], ncclDouble, root, s->comm, s->s_comm) != ncclSuccess)
-      status = fail(NLH_ERR_RCCL, "gather send");
-    if (hipStreamSynchronize(s->s_comm) != hipSuccess && status == NLH_OK)
-      status = fail(NLH_ERR_HIP, "gather sync");
-  } else {
-    std::vector<double> h(maxc);
-    for (int r = 0; r < s->p.nranks && status == NLH_OK; ++r) {
-      if (r == root || !count[r]) continue;
-      if (ncclRecv(buf, count[r], ncclDouble, r, s->comm, s->s_comm) != ncclSuccess) {
-        status = fail(NLH_ERR_RCCL, "gather recv");
-        break;
-      }
-      if (hipMemcpyAsync(h.data(), buf, count[r] * sizeof(double), hipMemcpyDeviceToHost, s->s_comm) != hipSuccess ||
-          hipStreamSynchronize(s->s_comm) != hipSuccess) {
-        status = fail(NLH_ERR_HIP, "gather copy");
-        break;
-      }
-      int64_t off = 0;
-      for (auto &b : s->plan.blocks) {
-        if (b.rank != r) continue;
-        for (int64_t y = 0; y < b.r.h; ++y)
-          std::memcpy(u + (b.r.y0 + y) * s->p.nx + b.r.x0, h.data() + off + y * b.r.w, b.r.w * sizeof(double));
-        off += b.r.w * b.r.h;
-      }
+  };
+  std::vector<double> h;
+  auto unpack = [&](int r) {
+    h.resize(count[r]);
+    if (hipMemcpyAsync(h.data(), rbuf, count[r] * sizeof(double), hipMemcpyDeviceToHost, s->s_comm) != hipSuccess ||
+        hipStreamSynchronize(s->s_comm) != hipSuccess) {
+      status = fail(NLH_ERR_HIP, "gather copy");
+      return;
     }
+    int64_t off = 0;
+    for (auto &b : s->plan.blocks) {
+      if (b.rank != r) continue;
+      for (int64_t y = 0; y < b.r.h; ++y)
+        std::memcpy(u + (b.r.y0 + y) * s->p.nx + b.r.x0, h.data() + off + y * b.r.w, b.r.w * sizeof(double));
+      off += b.r.w * b.r.h;
+    }
+  };
+  for (int r = 0; r < s->owners && status == NLH_OK; ++r) {
+    if (r == root || !count[r]) continue;
+    const bool sender = runs(s, r);
+    if (!sender && !at_root) continue;
+    if (sender) pack(r);
+    if (status != NLH_OK) break;
+    bool ok = ncclGroupStart() == ncclSuccess;
+    const int to = s->vranks ? 0 : root, from = s->vranks ? 0 : r;
+    if (sender) ok = ok && ncclSend(sbuf, count[r], ncclDouble, to, s->comm, s->s_comm) == ncclSuccess;
+    if (at_root) ok = ok && ncclRecv(rbuf, count[r], ncclDouble, from, s->comm, s->s_comm) == ncclSuccess;
+    ok = (ncclGroupEnd() == ncclSuccess) && ok;
+    if (!ok) {
+      status = fail(NLH_ERR_RCCL, "gather send/recv");
+      break;
+    }
+    if (at_root) unpack(r);
+    if (hipStreamSynchronize(s->s_comm) != hipSuccess && status == NLH_OK) status = fail(NLH_ERR_HIP, "gather sync");
   }
-  (void)hipFree(buf);
+  (void)hipFree(sbuf);
+  (void)hipFree(rbuf);
   return status;
 }
 
@@ -1362,15 +1498,19 @@ int nlh_run(nlh_solver *s, int64_t nsteps) {
     HIP_TRY(hipEventRecord(e0, s->s_main));
   }
   int64_t i = 0;
+  // busy timing records 2-4 event pairs per pass: fold them every kEvFold
+  // events inside one long call too, so the pool stays bounded
+  auto fold = [&] { return s->timing == 2 && s->ev_used >= kEvFold ? fold_events(s) : (int)NLH_OK; };
   if (s->pair)
     for (; i + 2 <= nsteps; i += 2)
-      if ((rc = enqueue_step(s, 2))) return rc;
+      if ((rc = enqueue_step(s, 2)) || (rc = fold())) return rc;
   for (; i < nsteps; ++i)
-    if ((rc = enqueue_step(s, 1))) return rc;
+    if ((rc = enqueue_step(s, 1)) || (rc = fold())) return rc;
   if (s->exchange) HIP_TRY(hipStreamWaitEvent(s->s_main, s->ev_band, 0));  // last bands
   if (e1) {
     HIP_TRY(hipEventRecord(e1, s->s_main));
     s->ev_steps.push_back((int)nsteps);
+    s->ev_owner.push_back(-1);
   }
   return NLH_OK;
 }
@@ -1406,10 +1546,23 @@ int nlh_errors(nlh_solver *s, int64_t time, double *l2, double *linf) {
     HIP_TRY(hipMemcpyAsync(h.data(), s->d_part, s->part_total * sizeof(nlh::NormPartial),
                            hipMemcpyDeviceToHost, s->s_main));
   HIP_TRY(hipStreamSynchronize(s->s_main));
+  // each (virtual) rank's partial sums over its blocks in block order, then
+  // across ranks: RCCL all-reduce between real ranks, rank order between the
+  // virtual ranks of this process (the self-communicator's all-reduce below
+  // is then the identity)
+  std::vector<double> e2r(s->owners, 0.0), eir(s->owners, 0.0);
+  for (size_t bi = 0; bi < s->blocks.size(); ++bi) {
+    const int o = s->blocks[bi].owner;
+    const int end = bi + 1 < s->blocks.size() ? s->part_off[bi + 1] : s->part_total;
+    for (int i = s->part_off[bi]; i < end; ++i) {
+      e2r[o] += h[i].l2;
+      eir[o] = std::max(eir[o], h[i].linf);
+    }
+  }
   double e2 = 0.0, ei = 0.0;
-  for (int i = 0; i < s->part_total; ++i) {
-    e2 += h[i].l2;
-    ei = std::max(ei, h[i].linf);
+  for (int r : s->mine) {
+    e2 += e2r[r];
+    ei = std::max(ei, eir[r]);
   }
   if (s->comm) {
     double v[2] = {e2, ei};
@@ -1442,8 +1595,7 @@ int nlh_get_info(const nlh_solver *s, nlh_info *info) {
   info->halo_width = s->halo;
   info->steps_per_pass = s->pair ? 2 : 1;
   info->owners = s->owners;
-  const char *pk = s->pair ? (s->pair_split == 3 ? "k_pair_pf" : s->pair_split == 2 ? "k_pair_mw"
-                              : (s->pair_split == 1 || s->pair_split == 6) ? "k_pair_split" : "k_pair")
+  const char *pk = s->pair ? "k_pair_split"
                            : s->wide ? "k_wide" : s->weighted ? "k_weighted"
                            : s->kernel == NLH_KERNEL_FAST ? "k_fast"
                            : nlh::exact_lds_ok((int)s->p.eps, s->p.test != 0) ? "k_exact_lds" : "k_exact";
@@ -1462,8 +1614,10 @@ int nlh_kernel_timing(nlh_solver *s, int enable) {
   s->timing = enable == 2 ? 2 : enable != 0 ? 1 : 0;
   s->ev_used = 0;
   s->ev_steps.clear();
+  s->ev_owner.clear();
   s->ev_acc_ms = 0.0;
   s->ev_acc_steps = 0;
+  s->ev_acc_owner.assign(s->owners, 0.0);
   return NLH_OK;
 }
 
@@ -1528,6 +1682,40 @@ int64_t nlh_halo_plan(const nlh_params *p, int64_t *pieces, int64_t cap) {
   }
   return n;
 }
+
+int64_t nlh_exchange_plan(const nlh_params *p, int64_t *out, int64_t cap) {
+  if (!p) return -fail(NLH_ERR_ARG, "null params");
+  const int64_t tx = p->tiles_x > 0 ? p->tiles_x : 1, ty = p->tiles_y > 0 ? p->tiles_y : 1;
+  if (p->nx <= 0 || p->ny <= 0 || p->nx % tx || p->ny % ty || p->nranks < 1 || p->rank < 0 ||
+      p->rank >= p->nranks)
+    return -fail(NLH_ERR_ARG, "bad lattice / tile grid / rank");
+  std::vector<int32_t> o;
+  std::string err;
+  if (!nlh::resolve_owner(tx, ty, p->nranks, p->owner, o, err)) return -fail(NLH_ERR_ARG, err);
+  Resolved rv;
+  if (int rc = resolve_config(*p, rv)) return -rc;
+  nlh::Plan plan = nlh::make_plan(p->nx, p->ny, rv.halo, tx, ty, o, p->split_tiles == 0);
+  const auto lay = nlh::exchange_layout(plan, p->rank, false);
+  for (size_t i = 0; out && i < lay.size() && (int64_t)i < cap; ++i) {
+    const auto &e = lay[i];
+    const nlh::Piece &pc = plan.pieces[e.piece];
+    int64_t *r = out + 8 * i;
+    r[0] = e.peer;
+    r[1] = e.dir;
+    r[2] = e.offset;
+    r[3] = pc.r.x0;
+    r[4] = pc.r.y0;
+    r[5] = pc.r.w;
+    r[6] = pc.r.h;
+    r[7] = e.piece;
+  }
+  return (int64_t)lay.size();
+}
+
+#ifndef NLH_BUILD_ID
+#error "NLH_BUILD_ID must be defined by the build (Makefile: hash of the library sources)"
+#endif
+const char *nlh_build_id(void) { return NLH_BUILD_ID; }
 
 int64_t nlh_block_plan(const nlh_params *p, int64_t *blocks, int64_t cap) {
   if (!p) return -fail(NLH_ERR_ARG, "null params");
@@ -1603,18 +1791,13 @@ int nlh_rebalance(nlh_solver *s, const double *busy_in, int32_t apply, int32_t *
     for (int r = 0; r < R; ++r) busy[r] = busy_in[r];
   } else {
     if (s->timing != 2) return -fail(NLH_ERR_STATE, "busy timing is off (nlh_kernel_timing(s, 2))");
-    double mine = 0.0;
-    if ((rc = local_busy(s, mine))) return -rc;
-    if (R != s->p.nranks) {
-      // NLH_VIRTUAL_RANKS: one GPU runs every owner; its measured busy time
-      // is apportioned by owned tiles (tiles are equal-sized)
-      std::vector<int64_t> cnt(R, 0);
-      for (int32_t v : s->owner) ++cnt[v];
-      for (int r = 0; r < R; ++r) busy[r] = mine * (double)cnt[r] / (double)s->owner.size();
-    } else {
-      busy[s->p.rank] = mine;
-    }
-    if (s->comm && R > 1 && R == s->p.nranks) {
+    std::vector<double> per;
+    if ((rc = owner_busy(s, per))) return -rc;
+    // virtual ranks: each one's own measured launch groups (their lists are
+    // launched and timed separately); a real rank: its own, then all-gathered
+    for (int r = 0; r < R; ++r) busy[r] = per[r];
+    const double mine = per[s->p.rank];
+    if (s->comm && R > 1 && R == s->p.nranks && !s->vranks) {
       double *d = nullptr;
       if (hipMalloc(&d, (R + 1) * sizeof(double)) != hipSuccess) return -fail(NLH_ERR_HIP, "busy buffer");
       int st = NLH_OK;

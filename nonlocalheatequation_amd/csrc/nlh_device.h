@@ -35,6 +35,8 @@ struct RectList {
   Rect r[kMaxRects];
   int32_t nrects;
   int32_t nwork;
+  int32_t owner;  // host bookkeeping: the (virtual) rank owning every rect of the list
+  int32_t pad_;
 };
 
 // Per-step constants.  All trig values are computed on the host with glibc
@@ -103,13 +105,10 @@ int launch_wide(const RectList &rl, const StepConst &c, bool test, void *stream)
 // two-step pass (nlh_pair.h): production mode, eps in [1, 16]
 bool pair_supported(int E);
 int pair_strip_width(int E);  // output columns per strip: 128 - 2E
-// variant: 0 k_pair (one wave), 1 k_pair_split (the two stages on two
-// waves), 2 k_pair_mw (plus a third wave for all HBM traffic)
+// variant: k_pair_split's ring configuration (nlh_pair.h: 1 / 6 production,
+// 5 / 4 test mode); all bitwise equal
 int pair_blocks_per_cu(int E, int variant);  // resident workgroups per CU (0 = unknown)
 int launch_pair(const RectList &rl, const StepConst &c, int variant, void *stream);
-int launch_pair_ablation(const RectList &rl, const StepConst &c, int abl, void *stream);
-// diagnostics (NLH_ABLATE=1|2, eps=8 only): see k_fast's ABL parameter
-int launch_fast_ablation(const RectList &rl, const StepConst &c, int abl, void *stream);
 int launch_exact(const RectList &rl, const StepConst &c, bool test, void *stream);
 // fast path for a non-constant J (influence != 0, eps <= 32): LDS tile of
 // 64 x 16 outputs per workgroup, direct weighted sum over the disk's 4-fold

@@ -21,7 +21,8 @@ namespace nlh {
 // columns, are co-resident on one XCD.
 constexpr int kFastD = 6;  // rows in flight per wave
 
-// ABL (diagnostics only, NLH_ABLATE): bit mask, 0 = production.  1 = no
+// ABL: timing-decomposition masks for the tools/ harness (tools/wide_bench.hip);
+// libnlh instantiates ABL = 0 only (results are meaningless otherwise).  1 = no
 // arithmetic (loads/stores kept, window values kept alive), 2 = no HBM traffic
 // (no DMA, no stores), 4 = no XCD remap, 8 = no alternating sweep, 16 = no
 // window LDS reads, 32 = plain (temporal) tail-chunk loads, 64 = plain loads
@@ -243,13 +244,6 @@ __global__ __launch_bounds__(64) void k_fast(RectList L, StepConst C) {
     bs = (bs + P) & (K - 1);
   }
   wait_vmcnt<0>();  // drain the clamped tail DMAs before the wave retires
-}
-
-template <int E, int R, int ABL, int D>
-int launch_fast_abl(const RectList &rl, const StepConst &c, hipStream_t st) {
-  hipLaunchKernelGGL((k_fast<E, R, D, false, ABL>), dim3(rl.nwork), dim3(64), 0, st, rl, c);
-  const hipError_t e = hipGetLastError();
-  return e == hipSuccess ? 0 : (int)e;
 }
 
 template <int E, int R, bool TEST>

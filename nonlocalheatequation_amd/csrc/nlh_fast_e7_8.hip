@@ -16,7 +16,4 @@ template int launch_fast_er<7, 1, true>(const RectList &, const StepConst &, hip
 template int launch_fast_er<7, 1, false>(const RectList &, const StepConst &, hipStream_t);
 template int launch_fast_er<8, 1, true>(const RectList &, const StepConst &, hipStream_t);
 template int launch_fast_er<8, 1, false>(const RectList &, const StepConst &, hipStream_t);
-template int launch_fast_abl<8, 2, 0, 6>(const RectList &, const StepConst &, hipStream_t);
-template int launch_fast_abl<8, 2, 1, 6>(const RectList &, const StepConst &, hipStream_t);
-template int launch_fast_abl<8, 2, 2, 6>(const RectList &, const StepConst &, hipStream_t);
 }  // namespace nlh

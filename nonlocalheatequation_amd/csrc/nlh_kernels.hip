@@ -568,22 +568,6 @@ int launch_wide(const RectList &rl, const StepConst &c, bool test, void *stream)
   }
 }
 
-extern template int launch_fast_abl<8, 2, 0, 6>(const RectList &, const StepConst &, hipStream_t);
-extern template int launch_fast_abl<8, 2, 1, 6>(const RectList &, const StepConst &, hipStream_t);
-extern template int launch_fast_abl<8, 2, 2, 6>(const RectList &, const StepConst &, hipStream_t);
-
-// NLH_ABLATE = 100 * k_fast ABL mask + prefetch distance (diagnostics, eps=8, R=2)
-int launch_fast_ablation(const RectList &rl, const StepConst &c, int abl, void *stream) {
-  if (c.E != 8) return -1;
-  hipStream_t st = (hipStream_t)stream;
-  switch (abl) {
-    case 6: return launch_fast_abl<8, 2, 0, 6>(rl, c, st);
-    case 106: return launch_fast_abl<8, 2, 1, 6>(rl, c, st);
-    case 206: return launch_fast_abl<8, 2, 2, 6>(rl, c, st);
-    default: return -1;
-  }
-}
-
 // Two-step pass (nlh_pair.h), instantiated in nlh_pair_e*.hip for E = 1..16
 #define NLH_PAIR_EXTERN(E) \
   extern template int launch_pair_e<E>(const RectList &, const StepConst &, int, hipStream_t); \
@@ -592,35 +576,6 @@ NLH_PAIR_EXTERN(1) NLH_PAIR_EXTERN(2) NLH_PAIR_EXTERN(3) NLH_PAIR_EXTERN(4)
 NLH_PAIR_EXTERN(5) NLH_PAIR_EXTERN(6) NLH_PAIR_EXTERN(7) NLH_PAIR_EXTERN(8)
 NLH_PAIR_EXTERN(9) NLH_PAIR_EXTERN(10) NLH_PAIR_EXTERN(11) NLH_PAIR_EXTERN(12)
 NLH_PAIR_EXTERN(13) NLH_PAIR_EXTERN(14) NLH_PAIR_EXTERN(15) NLH_PAIR_EXTERN(16)
-
-extern template int launch_pair_abl<8, 2, 7>(const RectList &, const StepConst &, hipStream_t);
-extern template int launch_pair_abl<8, 0, 6>(const RectList &, const StepConst &, hipStream_t);
-extern template int launch_pair_abl<8, 0, 5>(const RectList &, const StepConst &, hipStream_t);
-extern template int launch_pair_abl<8, 0, 3>(const RectList &, const StepConst &, hipStream_t);
-
-extern template int launch_pair_abl<8, 2, 8, true, 4>(const RectList &, const StepConst &, hipStream_t);
-extern template int launch_pair_abl<8, 0, 6, true, 1>(const RectList &, const StepConst &, hipStream_t);
-extern template int launch_pair_abl<8, 0, 6, true, 2>(const RectList &, const StepConst &, hipStream_t);
-extern template int launch_pair_abl<8, 0, 6, true, 4>(const RectList &, const StepConst &, hipStream_t);
-extern template int launch_pair_abl<8, 0, 10, true, 2>(const RectList &, const StepConst &, hipStream_t);
-// NLH_PAIR_ABLATE = 100 * k_pair ABL mask + prefetch distance (diagnostics, eps=8);
-// >= 10000: k_pair_split, 10000 + 1000 * ABL + 100 * B + D
-int launch_pair_ablation(const RectList &rl, const StepConst &c, int abl, void *stream) {
-  if (c.E != 8) return -1;
-  hipStream_t st = (hipStream_t)stream;
-  switch (abl) {
-    case 207: return launch_pair_abl<8, 2, 7>(rl, c, st);
-    case 6: return launch_pair_abl<8, 0, 6>(rl, c, st);
-    case 5: return launch_pair_abl<8, 0, 5>(rl, c, st);
-    case 3: return launch_pair_abl<8, 0, 3>(rl, c, st);
-    case 12408: return launch_pair_abl<8, 2, 8, true, 4>(rl, c, st);
-    case 10106: return launch_pair_abl<8, 0, 6, true, 1>(rl, c, st);
-    case 10206: return launch_pair_abl<8, 0, 6, true, 2>(rl, c, st);
-    case 10406: return launch_pair_abl<8, 0, 6, true, 4>(rl, c, st);
-    case 10210: return launch_pair_abl<8, 0, 10, true, 2>(rl, c, st);
-    default: return -1;
-  }
-}
 
 // E = 13 and 15 spill registers in k_pair_split under hipcc 7.2 (and k_pair
 // runs one wave per SIMD there): the single-step k_fast is faster for them

@@ -11,13 +11,4 @@ template int launch_pair_e<7>(const RectList &, const StepConst &, int, hipStrea
 template int pair_blocks_per_cu_e<7>(int);
 template int launch_pair_e<8>(const RectList &, const StepConst &, int, hipStream_t);
 template int pair_blocks_per_cu_e<8>(int);
-template int launch_pair_abl<8, 2, 7>(const RectList &, const StepConst &, hipStream_t);
-template int launch_pair_abl<8, 0, 6>(const RectList &, const StepConst &, hipStream_t);
-template int launch_pair_abl<8, 0, 5>(const RectList &, const StepConst &, hipStream_t);
-template int launch_pair_abl<8, 0, 3>(const RectList &, const StepConst &, hipStream_t);
-template int launch_pair_abl<8, 2, 8, true, 4>(const RectList &, const StepConst &, hipStream_t);
-template int launch_pair_abl<8, 0, 6, true, 1>(const RectList &, const StepConst &, hipStream_t);
-template int launch_pair_abl<8, 0, 6, true, 2>(const RectList &, const StepConst &, hipStream_t);
-template int launch_pair_abl<8, 0, 6, true, 4>(const RectList &, const StepConst &, hipStream_t);
-template int launch_pair_abl<8, 0, 10, true, 2>(const RectList &, const StepConst &, hipStream_t);
 }  // namespace nlh

@@ -5,6 +5,7 @@
 #include <cstdint>
 #include <cmath>
 #include <cstdlib>
+#include <map>
 
 namespace nlh {
 
@@ -301,6 +302,26 @@ int balance_owner(int64_t tiles_x, int64_t tiles_y, int32_t nranks,
     ++moved;
   }
   return moved;
+}
+
+std::vector<XferEntry> exchange_layout(const Plan &plan, int32_t me, bool self_all) {
+  std::vector<XferEntry> out;
+  std::map<int32_t, int64_t> soff, roff;
+  for (size_t i = 0; i < plan.pieces.size(); ++i) {
+    const Piece &pc = plan.pieces[i];
+    const bool remote = pc.src_rank != pc.dst_rank || (self_all && pc.src_rank == me);
+    if (!remote) continue;
+    const int64_t n = pc.r.w * pc.r.h;
+    if (pc.src_rank == me) {
+      out.push_back({pc.dst_rank, 0, (int32_t)i, soff[pc.dst_rank]});
+      soff[pc.dst_rank] += n;
+    }
+    if (pc.dst_rank == me) {
+      out.push_back({pc.src_rank, 1, (int32_t)i, roff[pc.src_rank]});
+      roff[pc.src_rank] += n;
+    }
+  }
+  return out;
 }
 
 }  // namespace nlh

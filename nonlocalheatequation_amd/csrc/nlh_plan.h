@@ -85,4 +85,22 @@ int balance_owner(int64_t tiles_x, int64_t tiles_y, int32_t nranks,
                   const std::vector<int32_t> &owner, const double *busy,
                   std::vector<int32_t> &owner_out);
 
+// One halo piece inside the RCCL message between `me` and `peer`: me packs it
+// into its send buffer for peer (dir 0) or unpacks it from its receive buffer
+// from peer (dir 1), `offset` doubles into that buffer, w*h doubles long.
+struct XferEntry {
+  int32_t peer = 0, dir = 0;
+  int32_t piece = 0;    // index into Plan::pieces
+  int64_t offset = 0;   // doubles
+};
+
+// The halo pieces rank `me` exchanges with other ranks, in plan order, with
+// their offsets in the per-peer messages (replaces the per-tile get_data_action
+// traffic of src/2d_nonlocal_distributed.cpp:1121-1131,1156-1259).  Both
+// sides walk Plan::pieces in the same order, so the offset of a piece in A's
+// send buffer for B equals its offset in B's receive buffer from A (tests:
+// tests/test_decomposition.py).  self_all: every piece with src_rank ==
+// dst_rank == me goes to itself as well (one-rank RCCL-to-self diagnostics).
+std::vector<XferEntry> exchange_layout(const Plan &plan, int32_t me, bool self_all);
+
 }  // namespace nlh

@@ -37,7 +37,39 @@ def test_python_binding_covers_header():
 
 
 def test_abi_version():
-    assert N.lib().nlh_abi_version() == 6
+    assert N.lib().nlh_abi_version() == 7
+
+
+def test_build_id_matches_sources():
+    # the library under test was built from this tree's sources and flags
+    assert N.build_id() == N.source_build_id()
+
+
+def test_no_diagnostic_kernels_in_library():
+    """libnlh ships only result-producing kernels: no ablation instance
+    (ABL != 0) of k_pair_split / k_fast / k_wide and none of the alternate
+    two-step designs (tools/pair_variants.h, harness only)."""
+    blob = open(N.lib_path(), "rb").read()
+    names = set(re.findall(rb"_ZN3nlh\d+k_\w+", blob))
+    assert any(b"k_pair_split" in n for n in names)
+    for n in names:
+        s = n.decode()
+        assert "k_pair_mw" not in s and "k_pair_pf" not in s and "6k_pairI" not in s, s
+        m = re.search(r"12k_pair_splitILi\d+ELi\d+ELi(\d+)E", s)
+        assert not m or m.group(1) == "0", s
+        m = re.search(r"6k_fastILi\d+ELi\d+ELi\d+ELb[01]ELi(\d+)E", s)
+        assert not m or m.group(1) == "0", s
+
+
+@pytest.mark.parametrize("var,val,msg", [("NLH_ABLATE", "1", "ablation"), ("NLH_PAIR_ABLATE", "12408", "ablation"),
+                                         ("NLH_PAIR_SPLIT", "2", "NLH_PAIR_SPLIT"),
+                                         ("NLH_SCHED", "7", "NLH_SCHED"), ("NLH_FAST_R", "x", "NLH_FAST_R")])
+def test_env_rejected_before_device(monkeypatch, var, val, msg):
+    # nlh_create validates the environment before it looks for a device, so
+    # no setting can make the product library compute something else
+    monkeypatch.setenv(var, val)
+    with pytest.raises(N.NLHError, match=msg):
+        N.Solver(50, 50, 5)
 
 
 def test_params_layout_matches_header():

@@ -155,3 +155,4 @@ def test_serial_linear_influence_flag(oracle):
     p = subprocess.run([os.path.join(BIN, "2d_nonlocal_serial"), "--influence", "quadratic"],
                        capture_output=True, text=True, timeout=60)
     assert p.returncode != 0
+

@@ -26,7 +26,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import ROOT, read_input
+from conftest import ROOT, read_input, virtual_peer_pairs
 
 import nonlocalheatequation_amd as N
 
@@ -71,19 +71,28 @@ def _run(nx, ny, eps, nt, kernel, u0=None, tiles=(1, 1), split=False, owner=None
         return s.field(), s.info()
 
 
-def test_c3_blocks_over_rccl_self(monkeypatch):
+@pytest.mark.parametrize("mode", ["rccl_self", "virtual8"])
+def test_c3_blocks_over_rccl_self(monkeypatch, mode):
     """C3's 2 x 4 layout of 16384 x 8192 blocks (8.6 GB per field) through the
-    RCCL transport, two two-step passes; vs k_exact per node, and linear."""
+    RCCL transport, two two-step passes; vs k_exact per node, and linear.
+    rccl_self: one rank, all eight blocks', every piece over RCCL to self;
+    virtual8: eight virtual ranks with one block each, each with its own
+    per-peer buffers (3-5 peers), every rank-to-rank message in one grouped
+    exchange -- the 8-GPU run's message pattern."""
     n, eps, nt = 32768, 8, 4
     rng = np.random.default_rng(3)
     u0 = np.empty((n, n))
     for y in range(0, n, 4096):
         u0[y:y + 4096] = rng.uniform(-1.0, 1.0, size=(4096, n))
-    monkeypatch.setenv("NLH_RCCL_SELF", "1")
+    env = ("NLH_RCCL_SELF", "1") if mode == "rccl_self" else ("NLH_VIRTUAL_RANKS", "8")
+    monkeypatch.setenv(*env)
     uf, info = _run(n, n, eps, nt, "fast", u0, tiles=(2, 4), split=True)
-    assert info.nblocks == 8 and info.npeers == 1 and info.steps_per_pass == 2
+    peers = 1 if mode == "rccl_self" else virtual_peer_pairs(n, n, eps, (2, 4), None, 8, split_tiles=True,
+                                                             dt=_dt(eps, 1.0 / n), dh=1.0 / n)
+    assert info.nblocks == 8 and info.npeers == peers and info.steps_per_pass == 2
+    assert mode == "rccl_self" or peers == 32  # 2x4 blocks: 4 corner ranks x 3 peers + 4 inner x 5
     assert info.halo_width == 2 * eps and info.halo_bytes_sent > 0
-    monkeypatch.delenv("NLH_RCCL_SELF")
+    monkeypatch.delenv(env[0])
     ue, info_e = _run(n, n, eps, nt, "exact", u0)
     assert info_e.kernel == N.KERNEL_EXACT and info_e.nblocks == 1
     d, scale = _max_abs_diff(uf, ue)
@@ -92,9 +101,33 @@ def test_c3_blocks_over_rccl_self(monkeypatch):
     # linearity of the explicit step (test=0): every add, multiply and fma of
     # the pass commutes with scaling by 2, so step(2u) == 2 step(u) bitwise
     u0 *= 2.0
-    monkeypatch.setenv("NLH_RCCL_SELF", "1")
+    monkeypatch.setenv(*env)
     u2, _ = _run(n, n, eps, nt, "fast", u0, tiles=(2, 4), split=True)
     assert _bitwise_double(uf, u2)
+
+
+@pytest.mark.parametrize("test", [False, True])
+def test_c4_run_length_wide_vs_exact(test):
+    """C4 at its run length: 100 steps (BASELINE C4: nt = 100) at 8192^2,
+    eps = 32, k_wide vs the bit-parity k_exact per node, 1e-12 of field
+    scale -- rounding drift of the prefix-sum windows over a whole run, in
+    production and test mode (test_init IC; L2 within 1e-10 relative)."""
+    n, eps, nt = 8192, 32, 100
+    dh = 1.0 / n
+    res = {}
+    for kernel in ("fast", "exact"):
+        with N.Solver(n, n, eps, 1.0, _dt(eps, dh), dh, test=test, kernel=kernel) as s:
+            s.test_init()
+            s.run(nt)
+            s.synchronize()
+            res[kernel] = (s.field(), s.errors(nt) if test else None, s.info())
+    uf, ef, info = res["fast"]
+    ue, ee, info_e = res["exact"]
+    assert info.pass_kernel == "k_wide" and info_e.kernel == N.KERNEL_EXACT
+    d, scale = _max_abs_diff(uf, ue)
+    assert d <= 1e-12 * scale, f"max |diff| {d} vs scale {scale}"
+    if test:
+        assert abs(ef[0] - ee[0]) <= 1e-10 * ee[0]
 
 
 @pytest.mark.parametrize("tiles", [(1, 1), (2, 2), (2, 4)])
@@ -140,7 +173,8 @@ def test_c5_uneven_owner_map_virtual_ranks(monkeypatch):
     monkeypatch.setenv("NLH_VIRTUAL_RANKS", "8")
     uf, info = _run(n, n, eps, nt, "fast", None, tiles=(npx, npy), owner=owner)
     plan = N.block_plan(n, n, eps, (npx, npy), owner, 8, False)
-    assert info.nblocks == len(plan) > 8 and info.npeers == 1 and info.halo_bytes_sent > 0
+    pairs = virtual_peer_pairs(n, n, eps, (npx, npy), owner, 8, dt=_dt(eps, 1.0 / n), dh=1.0 / n)
+    assert info.nblocks == len(plan) > 8 and info.npeers == pairs > 8 and info.halo_bytes_sent > 0
     assert info.steps_per_pass == 2
     monkeypatch.delenv("NLH_VIRTUAL_RANKS")
     ue, _ = _run(n, n, eps, nt, "exact", None)

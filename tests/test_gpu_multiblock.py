@@ -15,6 +15,8 @@ import os
 import numpy as np
 import pytest
 
+from conftest import virtual_peer_pairs
+
 import nonlocalheatequation_amd as N
 
 pytestmark = pytest.mark.gpu
@@ -219,7 +221,7 @@ def test_snapshot_overlaps_later_steps(oracle, tiles, split, kernel):
 
 
 def _owner_25s_8n():
-    from conftest import read_input
+    from conftest import virtual_peer_pairs, read_input
     tok = read_input("load_balance_25s_8n.txt").split()
     npx, npy = int(tok[2]), int(tok[3])
     own = [0] * (npx * npy)
@@ -245,7 +247,9 @@ def test_virtual_ranks_uneven_map(oracle, monkeypatch, kernel, test, nt):
     u0 = None if test else rng.uniform(-1, 1, size=(ny, nx))
     u, (l2, li), info, (k, dt, dh) = _run(nx, ny, eps, nt, test, kernel, (5, 5), False, owner=owner, u0=u0)
     plan = N.block_plan(nx, ny, eps, (5, 5), owner, 8, False)
-    assert info.nblocks == len(plan) > 8 and info.npeers == 1 and info.halo_bytes_sent > 0
+    # every virtual rank with its own per-peer buffers: the grouped multi-peer exchange
+    pairs = virtual_peer_pairs(nx, ny, eps, (5, 5), owner, 8, test=test, kernel=kernel, k=k, dt=dt, dh=dh)
+    assert info.nblocks == len(plan) > 8 and info.npeers == pairs > 8 and info.halo_bytes_sent > 0
     p = oracle.params(nx, ny, eps, k, dt, dh, int(test))
     ref = oracle.run(p, nt, u0)
     if kernel == "exact":
@@ -253,3 +257,38 @@ def test_virtual_ranks_uneven_map(oracle, monkeypatch, kernel, test, nt):
         assert li == oracle.errors(p, nt, ref)[1]
     else:
         assert np.max(np.abs(u - ref)) <= 1e-12 * np.max(np.abs(ref))
+
+
+@pytest.mark.parametrize("kernel,test", [("exact", True), ("fast", True), ("fast", False)])
+@pytest.mark.parametrize("root", [0, 3])
+def test_virtual_ranks_gather_and_errors(oracle, monkeypatch, kernel, test, root):
+    """Under NLH_VIRTUAL_RANKS every rank's blocks travel to the root over
+    RCCL (to self) in its own plan-ordered message, as nlh_gather_field does
+    between real ranks (the reference pulls every tile to locality 0,
+    src/2d_nonlocal_distributed.cpp:496,1121-1131); the error norms are summed
+    per rank first, then over ranks (:495-520)."""
+    monkeypatch.setenv("NLH_VIRTUAL_RANKS", "8")
+    owner = _owner_25s_8n()
+    nx = ny = 5 * 40
+    eps, nt = 5, 5
+    dh = 1.0 / nx
+    dt = eps ** 4 * dh * dh / (8 * N.disk_count(eps))
+    with N.Solver(nx, ny, eps, 1.0, dt, dh, test=test, kernel=kernel, tiles=(5, 5), owner=owner) as s:
+        s.test_init()
+        s.run(nt)
+        s.synchronize()
+        u = s.field()
+        g = s.gather(root)
+        l2, li = s.errors(nt)
+        assert s.info().owners == 8
+    assert np.array_equal(g, u)
+    p = oracle.params(nx, ny, eps, 1.0, dt, dh, int(test))
+    ref = oracle.run(p, nt)
+    rl2, rli = oracle.errors(p, nt, ref)
+    if kernel == "exact":
+        assert np.array_equal(u, ref) and li == rli
+        assert l2 == pytest.approx(rl2, rel=1e-13)
+    else:
+        assert np.max(np.abs(u - ref)) <= 1e-12 * np.max(np.abs(ref))
+        if test:
+            assert l2 == pytest.approx(rl2, rel=1e-10)

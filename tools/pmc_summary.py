@@ -7,7 +7,10 @@ gfx950 correction (MI355X_MICROARCH.md 'HBM'): FETCH_SIZE reports exactly half
 the bytes of wide coalesced streaming reads -> doubled here; WRITE_SIZE is
 exact for 16-B-per-lane stores.  SQ_* are per dispatch, summed over the chip.
 
-    python tools/pmc_summary.py DIR KERNEL [--workload KEY --node-updates N --commit SHA]
+    python tools/pmc_summary.py DIR KERNEL [--workload KEY --node-updates N --commit SHA --build-id ID]
+
+--build-id: the libnlh build id of the profiled run (bench.py uses a
+committed record only when it equals the loaded library's).
 
 KERNEL is the short kernel name (k_pair_split, k_wide, k_fast, k_exact); it
 is matched against rocprofv3's demangled names as "KERNEL<".
@@ -27,6 +30,7 @@ def main():
     ap.add_argument("--workload", default=None)
     ap.add_argument("--node-updates", type=float, default=None, help="node-updates per launch")
     ap.add_argument("--commit", default=None)
+    ap.add_argument("--build-id", default=None)
     a = ap.parse_args()
     key = a.kernel + "<"
     vals, durs = {}, []
@@ -39,7 +43,7 @@ def main():
             if key in row["Kernel_Name"]:
                 durs.append(int(row["End_Timestamp"]) - int(row["Start_Timestamp"]))
     med = {k: statistics.median(v) for k, v in vals.items()}
-    out = {"kernel_match": a.kernel, "workload": a.workload, "commit": a.commit,
+    out = {"kernel_match": a.kernel, "workload": a.workload, "commit": a.commit, "build_id": a.build_id,
            "dispatches_per_counter": {k: len(v) for k, v in vals.items()}, "median": med}
     if "FETCH_SIZE" in med and "WRITE_SIZE" in med:
         rd = 2.0 * med["FETCH_SIZE"] * 1024
