@@ -88,7 +88,7 @@ __device__ __forceinline__ void dma_chunks(const double *g, uint32_t lds,
 
 // f(integral_constant<int, I>) for I = 0 .. N-1, fully unrolled
 template <int N, int I = 0, class F>
-__device__ __forceinline__ void static_for(F &f) {
+__device__ __forceinline__ void static_for(F &&f) {
   if constexpr (I < N) {
     f(std::integral_constant<int, I>{});
     static_for<N, I + 1>(f);

@@ -104,8 +104,18 @@ __device__ __forceinline__ double wave_prefix_sum(double x) {
 // per level.  The difference of two prefix sums of at most 160 values rounds at ~2^-45 of the
 // row's magnitude: far inside the 1e-12 field-scale tolerance once alpha ~ 1/N
 // scales the disk sum.
+//
+// PSPLIT (with PS): the two prefix reads of a level as separate ds_read_b64
+// (2 LDS cycles each); left alone the compiler pairs them into one
+// ds_read2_b64, which takes 8 (MI355X_MICROARCH.md LDS table)
+//
+// PA (with PS): prefix rows built PA rows ahead into a ring of PK prefix
+// slots -- row i's 38 window reads hit a prefix row finished PA rows earlier,
+// and the scan of row i+PA (its DPP chain and LDS write) is independent of
+// row i's window sums, so the two interleave instead of serialising each row
+// on scan -> LDS write -> LDS read.  Same arithmetic: bitwise equal to PA = 0.
 template <int E, int CH, bool TEST, int D = kWideD, int ABL = 0, int PIN = 1, bool AB = false, int OBP = 16,
-          bool SPLIT8 = true, bool PS = false>
+          bool SPLIT8 = true, bool PS = false, int PA = 0, bool PSPLIT = false>
 __global__ __launch_bounds__(64, 1) void k_wide(RectList L, StepConst C) {
   constexpr int W = 64;                 // output columns per strip
   constexpr int EP = (E + 1) & ~1;      // staged halo columns per side (16-B rows)
@@ -126,7 +136,10 @@ __global__ __launch_bounds__(64, 1) void k_wide(RectList L, StepConst C) {
   static_assert(CH % PIN == 0, "rows per pin");
 
   static_assert(!PS || (RW <= 256 && !AB), "prefix-sum rows: at most four staged doubles per lane");
-  constexpr int NP = PS ? RW + 2 : 0;  // prefix row: pfx[1] = 0, pfx[2 + k] = P(k)
+  static_assert(PA == 0 || (PS && PA < D), "prefix-ahead rows need prefix sums and landed rows");
+  constexpr int PK = PA ? pow2_ceil(PA + 1) : 1;  // prefix-row slots
+  constexpr int NPR = RW + 2;                      // doubles per prefix slot (16-B multiple)
+  constexpr int NP = PS ? PK * NPR : 0;  // prefix row: pfx[1] = 0, pfx[2 + k] = P(k)
   __shared__ __attribute__((aligned(16))) double ring[K * RWS + (TEST ? K * W + 2 * K : 0) + NP];
   double *lwr = ring + K * RWS;  // L_h[W0] rows (TEST), same slots as the u rows
   double *syr = lwr + K * W;     // sin(2 pi y dh) pairs (TEST), same slots
@@ -134,7 +147,7 @@ __global__ __launch_bounds__(64, 1) void k_wide(RectList L, StepConst C) {
 
   const int lane = (int)threadIdx.x;
   if constexpr (PS) {
-    if (lane == 0) pfx[1] = 0.0;  // P(-1); the row writes start at pfx[2]
+    if (lane < PK) pfx[lane * NPR + 1] = 0.0;  // P(-1) of every slot; the row writes start at [2]
   }
   const int work = xcd_remap(blockIdx.x, gridDim.x);
   const int ri = find_rect(L, work);
@@ -195,6 +208,37 @@ __global__ __launch_bounds__(64, 1) void k_wide(RectList L, StepConst C) {
 #pragma unroll
   for (int s = 0; s < D; ++s) issue();
 
+  // PS: prefix row of staged row r into prefix slot r mod PK
+  auto scan_row = [&](int r) __attribute__((always_inline)) {
+    const double *srow = ring + (r & (K - 1)) * RWS;
+    double *dst = pfx + (r & (PK - 1)) * NPR + 2;
+    double2 ab = make_double2(0.0, 0.0);
+    if (2 * lane < RW) ab = *reinterpret_cast<const double2 *>(srow + 2 * lane);
+    double2 cd = make_double2(0.0, 0.0);  // second chunk of the lane (E > 32)
+    if constexpr (RW > 128)
+      if (2 * (lane + 64) < RW) cd = *reinterpret_cast<const double2 *>(srow + 2 * (lane + 64));
+    const double sv = wave_prefix_sum(ab.x + ab.y);
+    double sw = 0.0;
+    if constexpr (RW > 128) {
+      const double tot = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(sv), 63),
+                                          __builtin_amdgcn_readlane(__double2loint(sv), 63));
+      sw = wave_prefix_sum(cd.x + cd.y) + tot;
+    }
+    asm volatile("" ::: "memory");
+    if (2 * lane < RW) *reinterpret_cast<double2 *>(dst + 2 * lane) = make_double2(sv - ab.y, sv);
+    if constexpr (RW > 128)
+      if (2 * (lane + 64) < RW) *reinterpret_cast<double2 *>(dst + 2 * (lane + 64)) = make_double2(sw - cd.y, sw);
+    asm volatile("" ::: "memory");  // in order per wave: later reads see every lane's write
+  };
+  if constexpr (PA > 0) {
+    // prologue: prefix rows 0 .. PA-1 (row r landed: D-1-r rows may still fly)
+    static_for<PA>([&](auto rc) __attribute__((always_inline)) {
+      constexpr int r = decltype(rc)::value;
+      wait_vmcnt<(D - 1 - r) * G>();
+      scan_row(r);
+    });
+  }
+
   double acc[NA];
 #pragma unroll
   for (int a = 0; a < NA; ++a) acc[a] = 0.0;
@@ -209,15 +253,16 @@ __global__ __launch_bounds__(64, 1) void k_wide(RectList L, StepConst C) {
       if constexpr ((ABL & 1) != 0) __builtin_amdgcn_sched_barrier(0);
       const int i = ibase + c;
       issue();  // input row i + D
-      // row i landed.  Issued after its DMA: the DMAs of rows i+1 .. i+D,
-      // and for c < D the CH output stores of the previous chunk's end
-      if constexpr (c < D) {
+      // row i + PA landed.  Issued after its DMA: the DMAs of rows
+      // i+PA+1 .. i+D, and for c + PA < D the CH output stores of the
+      // previous chunk's end
+      if constexpr (c + PA < D) {
         if (full)
-          wait_vmcnt<D * G + CH>();
+          wait_vmcnt<(D - PA) * G + CH>();
         else
-          wait_vmcnt<D * G>();
+          wait_vmcnt<(D - PA) * G>();
       } else {
-        wait_vmcnt<D * G>();
+        wait_vmcnt<(D - PA) * G>();
       }
       // this lane's window: staged columns xl-E .. xl+E
       // this lane's window w[0 .. 2E] (w[E] its own column).  AB: read as
@@ -283,7 +328,35 @@ __global__ __launch_bounds__(64, 1) void k_wide(RectList L, StepConst C) {
         }
       };
       const double wc = AB ? ((E % 2 == 0) ? wpair(E / 2).x : wpair(E / 2).y) : wrow[E];
-      if constexpr (PS) {
+      if constexpr (PS && PA > 0) {
+        // row i's prefix row was built PA rows ago: its window reads go out
+        // first, the scan of row i + PA runs while they are in flight
+        const double *pl = pfx + (i & (PK - 1)) * NPR + 2 + EP + lane;  // P(centre + k) at pl[k]
+        double hp[E + 1], hm[E + 1];
+        static_for<E>([&](auto lc) __attribute__((always_inline)) {
+          constexpr int Lv = decltype(lc)::value + 1;
+          if constexpr (wide_taps(E, Lv) > 0) {
+            hp[Lv] = pl[Lv];
+            if constexpr (PSPLIT) asm volatile("" ::: "memory");
+            hm[Lv] = pl[-Lv - 1];
+            if constexpr (PSPLIT) asm volatile("" ::: "memory");
+          }
+        });
+        asm volatile("" ::: "memory");  // the reads above are issued before the scan's write
+        scan_row(i + PA);
+        acc[c + 2 * E] = wc;
+        acc[c] += wc;
+        static_for<E>([&](auto lc) __attribute__((always_inline)) {
+          constexpr int Lv = decltype(lc)::value + 1;
+          if constexpr (wide_taps(E, Lv) > 0) {
+            const double h = hp[Lv] - hm[Lv];
+            static_for<wide_taps(E, Lv)>([&](auto kk) __attribute__((always_inline)) {
+              constexpr int dy = wide_tap_dy(E, Lv, decltype(kk)::value);
+              acc[c + E - dy] += h;
+            });
+          }
+        });
+      } else if constexpr (PS) {
         // prefix row of the staged row (slot i), then the used levels' windows
         const double *srow = ring + (i & (K - 1)) * RWS;
         double2 ab = make_double2(0.0, 0.0);
@@ -310,7 +383,11 @@ __global__ __launch_bounds__(64, 1) void k_wide(RectList L, StepConst C) {
         auto plevel = [&](auto lc) __attribute__((always_inline)) {
           constexpr int Lv = decltype(lc)::value + 1;
           if constexpr (wide_taps(E, Lv) > 0) {
-            const double h = pl[Lv] - pl[-Lv - 1];
+            const double ph = pl[Lv];
+            if constexpr (PSPLIT) asm volatile("" ::: "memory");
+            const double pm = pl[-Lv - 1];
+            if constexpr (PSPLIT) asm volatile("" ::: "memory");
+            const double h = ph - pm;
             auto tap = [&](auto kk) __attribute__((always_inline)) {
               constexpr int dy = wide_tap_dy(E, Lv, decltype(kk)::value);
               acc[c + E - dy] += h;
@@ -423,9 +500,21 @@ constexpr int wide_chunk() { return E <= 32 ? kWideC : 8; }
 template <int E>
 constexpr bool wide_ps() { return E <= 35; }
 
+// prefix-sum rows (E <= 35) are built two rows ahead of their window reads,
+// each read a separate ds_read_b64, in 8-row chunks: C4 (8192^2, eps 32)
+// 139.5 -> 155.8 G node/s in tools/wide_bench.hip, bitwise equal
+// (profiles/r03/wide_pa_sweep.jsonl)
+// (E <= 32: 146-251 VGPRs, two waves per SIMD; at 33-35 the prefetched
+// windows would take 256-274 and one wave per SIMD, so those keep PA = 0)
+template <int E>
+constexpr int wide_pa() { return E <= 32 ? 2 : 0; }
+template <int E>
+constexpr int wide_chunk_pa() { return E <= 32 ? 8 : wide_chunk<E>(); }
+
 template <int E, bool TEST>
 int launch_wide_e(const RectList &rl, const StepConst &c, hipStream_t st) {
-  hipLaunchKernelGGL((k_wide<E, wide_chunk<E>(), TEST, kWideD, 0, 1, false, 16, true, wide_ps<E>()>),
+  hipLaunchKernelGGL((k_wide<E, wide_chunk_pa<E>(), TEST, kWideD, 0, 1, false, 16, true, wide_ps<E>(), wide_pa<E>(),
+                             (wide_pa<E>() > 0)>),
                      dim3(rl.nwork), dim3(64), 0, st, rl, c);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : (int)e;
@@ -437,7 +526,9 @@ template <int E>
 int wide_blocks_per_cu_e() {
   int n = 0;
   const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-      &n, k_wide<E, wide_chunk<E>(), false, kWideD, 0, 1, false, 16, true, wide_ps<E>()>, 64, 0);
+      &n, k_wide<E, wide_chunk_pa<E>(), false, kWideD, 0, 1, false, 16, true, wide_ps<E>(), wide_pa<E>(),
+             (wide_pa<E>() > 0)>,
+      64, 0);
   return e == hipSuccess ? n : 0;
 }
 

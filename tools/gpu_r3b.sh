@@ -7,3 +7,4 @@ timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.
 timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench20.json 2> $O/bench20.err && \
 timeout -k 10 200 python bench.py --gpus 1 --steps 20 --warmup 5 --warmup-ms 0 --pmc off --no-cpu-baseline > $O/bench20_nowarm.json 2> $O/bench20_nowarm.err && \
 timeout -k 10 200 python bench.py --gpus 1 --steps 1000 --warmup 20 --pmc off --no-cpu-baseline > $O/bench1000.json 2> $O/bench1000.err
+
