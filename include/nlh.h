@@ -59,8 +59,9 @@ enum nlh_influence { NLH_INFLUENCE_CONSTANT = 0, NLH_INFLUENCE_LINEAR = 1 };
 /* Stencil implementation.  EXACT reproduces the reference's per-term
  * floating-point order bit for bit (4 ops per neighbour; ((J c)(u_j - u_i))
  * dh^2 with J from a per-offset table when J != 1).  FAST computes the
- * same J=1 disk sum by nested (eps <= 16, 36..48) or prefix-sum (17..35) row
- * windows (~4*eps adds per node; eps 49..52 a direct LDS-tile sum) and, in test
+ * same J=1 disk sum by nested (eps <= 16, 36..48) or prefix-sum (17..35 and,
+ * with a run-time horizon in two passes, 49..64) row windows (~4*eps adds
+ * per node) and, in test
  * mode, the manufactured source from a precomputed L_h[W0] field; it differs
  * from the reference only by summation rounding (<= 1e-12 of field scale per
  * node, L2 error within 1e-10).  AUTO = FAST wherever it is instantiated

@@ -138,13 +138,14 @@ def test_eps32_golden(kernel, test):
         assert np.max(np.abs(u - g)) <= 1e-12 * np.max(np.abs(g))
 
 
-@pytest.mark.parametrize("eps", [49, 52])
+@pytest.mark.parametrize("eps", [49, 52, 53, 57, 64])
 @pytest.mark.parametrize("test", [False, True])
-def test_large_eps_weighted_j1(oracle, eps, test):
-    """eps 49..52 (beyond the nested-window kernels): AUTO/FAST run k_weighted
-    with J = 1 over an LDS tile; per node within 1e-12 of field scale (the
-    north star's tolerance, no allowance), L2 as the oracle's; EXACT stays
-    bitwise."""
+def test_large_eps_runtime_horizon(oracle, eps, test):
+    """eps 49..64 (past the compile-time k_wide instances): AUTO/FAST run
+    k_wide_rt -- prefix-sum row windows at run-time offsets, the disk's row
+    offsets split over two passes; per node within 1e-12 of field scale (no
+    allowance), L2 as the oracle's; EXACT stays bitwise.  Ragged lattice
+    narrower than two strips, segments shorter than the horizon."""
     nx, ny, nt = 150, 133, 3
     dh = 1.0 / nx
     r = N.BatchRow(nx, ny, nt, eps, 1.0, 0.5 * eps ** 4 * dh * dh / (8 * N.disk_count(eps)), dh)
@@ -152,7 +153,7 @@ def test_large_eps_weighted_j1(oracle, eps, test):
     p = oracle.params(nx, ny, eps, r.k, r.dt, dh, int(test))
     ref = oracle.run(p, nt, u0)
     u, (l2, _), info = _gpu_run_j(r, test, "auto", "constant", u0)
-    assert info.pass_kernel == "k_weighted" and info.kernel == N.KERNEL_FAST
+    assert info.pass_kernel == "k_wide" and info.kernel == N.KERNEL_FAST
     d = np.max(np.abs(u - ref))
     scale = np.max(np.abs(ref))
     assert d <= 1e-12 * scale, d
@@ -164,7 +165,29 @@ def test_large_eps_weighted_j1(oracle, eps, test):
     assert info.kernel == N.KERNEL_EXACT and np.array_equal(ue, ref)
 
 
-@pytest.mark.parametrize("eps", [53, 64])
+@pytest.mark.parametrize("eps", [56, 64])
+@pytest.mark.parametrize("tiles", [(1, 1), (3, 2)])
+def test_large_eps_runtime_horizon_blocks(oracle, monkeypatch, eps, tiles):
+    """k_wide_rt through the multi-block exchange (RCCL to self) and over
+    several segments per strip, production mode, vs the oracle."""
+    if tiles != (1, 1):
+        monkeypatch.setenv("NLH_RCCL_SELF", "1")
+    nx, ny, nt = 192, 180, 3
+    dh = 1.0 / nx
+    dt = 0.7 * eps ** 4 * dh * dh / (8 * N.disk_count(eps))
+    u0 = np.random.default_rng(eps + 1).uniform(-1, 1, size=(ny, nx))
+    ref = oracle.run(oracle.params(nx, ny, eps, 1.0, dt, dh, 0), nt, u0)
+    with N.Solver(nx, ny, eps, 1.0, dt, dh, kernel="fast", tiles=tiles, split_tiles=tiles != (1, 1),
+                  seg_rows=70) as s:
+        s.input_init(u0)
+        s.run(nt)
+        s.synchronize()
+        u = s.field()
+        assert s.info().pass_kernel == "k_wide"
+    assert np.max(np.abs(u - ref)) <= 1e-12 * np.max(np.abs(ref))
+
+
+@pytest.mark.parametrize("eps", [65, 80])
 def test_unsupported_fast_eps_falls_back_to_exact(oracle, eps):
     r = N.BatchRow(60, 50, 2, eps, 1.0, 1e-4, 1.0 / 60)
     with N.Solver(r.nx, r.ny, eps, r.k, r.dt, r.dh, test=False, kernel="auto") as s:
