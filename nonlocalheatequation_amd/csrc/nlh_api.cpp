@@ -377,74 +377,94 @@ int build_rectlists(nlh_solver *s, int kind) {
       (r.interior ? inter : bnd).push_back(it);
     }
   }
-  // segment height for the fast kernel: ~1024 single-wave workgroups (4 per CU,
-  // all resident at once; balanced grids measured fastest, profiles/r01/tune_*.json)
-  int seg_h = 4;
-  if (fast) {
-    int64_t strip_rows = 0;
-    for (auto &it : all) strip_rows += ceil_div(it.r.x1 - it.r.x0, sw) * (it.r.y1 - it.r.y0);
-    const bool own = s->p.seg_rows > 0 && pair == s->pair;  // seg_rows tunes the kernel nlh_run uses most
-    if (pair) {
-      // k_pair: every resident wave (2 per SIMD at E = 8); k_pair_split: 4
-      // workgroups (8 waves) per CU -- taller segments beat more waves
-      // (profiles/r01/tune_v3b).  Segment height: minimise rounds x sweep,
-      // a sweep costing seg + 3E rows (stage 1 reads seg + 4E rows, stage 2
-      // seg + 2E); at 4096^2 this picks 152 rows = 999 workgroups in one
-      // round, the measured optimum; on large lattices several rounds of
-      // shorter segments instead of one round with idle slots
-      const int per_cu = std::max(1, nlh::pair_blocks_per_cu(E, s->p.test ? s->pair_test : s->pair_split));
-      int use_cu = s->pair_split != 0 ? std::min(per_cu, s->pair_cu) : per_cu;
-      // with an exchange the interior may be sized for fewer slots per CU,
-      // leaving room for the bands and RCCL beside it (NLH_INT_PER_CU)
-      // -- measured a win up to 4096^2-sized blocks (166 vs 182 us/step for
-      // four 4096^2 blocks over RCCL), a loss on the 16384 x 8192 share of C3
-      int64_t big = 0;
-      for (auto &b : s->blocks) big = std::max<int64_t>(big, b.r.w * b.r.h);
-      if (s->exchange_planned && s->int_per_cu > 0 && big <= (int64_t)4096 * 8192)
-        use_cu = std::min(use_cu, s->int_per_cu);
-      const int64_t resident = (int64_t)use_cu * s->cus;
-      const std::vector<Item> &sized = inter.empty() ? all : inter;
-      int64_t hmax = 1;
-      for (auto &it : sized) hmax = std::max<int64_t>(hmax, it.r.y1 - it.r.y0);
-      int64_t best = -1, best_cost = 0;
-      for (int64_t n = 1; n <= 1024; ++n) {
-        const int64_t seg = std::max<int64_t>(16, ceil_div(hmax, n));
-        int64_t wgs = 0;
-        for (auto &it : sized) wgs += ceil_div(it.r.x1 - it.r.x0, sw) * ceil_div(it.r.y1 - it.r.y0, seg);
-        const int64_t cost = ceil_div(wgs, resident) * (seg + 3 * E);
-        if (best < 0 || cost < best_cost) {
-          best = seg;
-          best_cost = cost;
+  // Segment heights (interior, bands) for a set of rects sized as ONE rank's
+  // launch on the whole GPU.  Virtual ranks are sized each for itself, as
+  // each would be on its own GPU: then each one's launches fill the device and
+  // its measured busy time follows its own work (load balancing).
+  auto sizes = [&](const std::vector<Item> &all, const std::vector<Item> &inter,
+                   const std::vector<Item> &bnd) -> std::pair<int, int> {
+    // segment height for the fast kernel: ~1024 single-wave workgroups (4 per CU,
+    // all resident at once; balanced grids measured fastest, profiles/r01/tune_*.json)
+    int seg_h = 4;
+    if (fast) {
+      int64_t strip_rows = 0;
+      for (auto &it : all) strip_rows += ceil_div(it.r.x1 - it.r.x0, sw) * (it.r.y1 - it.r.y0);
+      const bool own = s->p.seg_rows > 0 && pair == s->pair;  // seg_rows tunes the kernel nlh_run uses most
+      if (pair) {
+        // k_pair_split: 4 workgroups (8 waves) per CU -- taller segments beat
+        // more waves (profiles/r01/tune_v3b).  Segment height: minimise rounds
+        // x sweep, a sweep costing seg + 3E rows (stage 1 reads seg + 4E rows,
+        // stage 2 seg + 2E); at 4096^2 this picks 152 rows = 999 workgroups in
+        // one round, the measured optimum; on large lattices several rounds of
+        // shorter segments instead of one round with idle slots
+        const int per_cu = std::max(1, nlh::pair_blocks_per_cu(E, s->p.test ? s->pair_test : s->pair_split));
+        int use_cu = std::min(per_cu, s->pair_cu);
+        // with an exchange the interior may be sized for fewer slots per CU,
+        // leaving room for the bands and RCCL beside it (NLH_INT_PER_CU)
+        // -- measured a win up to 4096^2-sized blocks (166 vs 182 us/step for
+        // four 4096^2 blocks over RCCL), a loss on the 16384 x 8192 share of C3
+        int64_t big = 0;
+        for (auto &it : all) big = std::max<int64_t>(big, s->blocks[it.blk].r.w * s->blocks[it.blk].r.h);
+        if (s->exchange_planned && s->int_per_cu > 0 && big <= (int64_t)4096 * 8192)
+          use_cu = std::min(use_cu, s->int_per_cu);
+        const int64_t resident = (int64_t)use_cu * s->cus;
+        const std::vector<Item> &sized = inter.empty() ? all : inter;
+        int64_t hmax = 1;
+        for (auto &it : sized) hmax = std::max<int64_t>(hmax, it.r.y1 - it.r.y0);
+        int64_t best = -1, best_cost = 0;
+        for (int64_t n = 1; n <= 1024; ++n) {
+          const int64_t seg = std::max<int64_t>(16, ceil_div(hmax, n));
+          int64_t wgs = 0;
+          for (auto &it : sized) wgs += ceil_div(it.r.x1 - it.r.x0, sw) * ceil_div(it.r.y1 - it.r.y0, seg);
+          const int64_t cost = ceil_div(wgs, resident) * (seg + 3 * E);
+          if (best < 0 || cost < best_cost) {
+            best = seg;
+            best_cost = cost;
+          }
+          if (seg == 16) break;
         }
-        if (seg == 16) break;
+        seg_h = own ? s->p.seg_rows : (int)best;
+      } else if (s->wide) {
+        // k_wide: one-wave workgroups, all resident in one round: two waves per
+        // SIMD up to E = 40 (8 per CU, 214 VGPRs at E = 32;
+        // profiles/r02/wide_bench_*), one beyond (4 per CU)
+        const int per_cu = std::max(1, std::min(8, nlh::wide_blocks_per_cu(E)));
+        seg_h = own ? s->p.seg_rows
+                    : (int)std::max<int64_t>(2 * E, ceil_div(strip_rows, (int64_t)per_cu * s->cus));
+      } else {
+        seg_h = own ? s->p.seg_rows
+                    : (int)std::max<int64_t>(nlh::fast_seg_min(E), ceil_div(strip_rows, 1024));
       }
-      seg_h = own ? s->p.seg_rows : (int)best;
-    } else if (s->wide) {
-      // k_wide: one-wave workgroups, all resident in one round: two waves per
-      // SIMD up to E = 40 (8 per CU, 214 VGPRs at E = 32;
-      // profiles/r02/wide_bench_*), one beyond (4 per CU)
-      const int per_cu = std::max(1, std::min(8, nlh::wide_blocks_per_cu(E)));
-      seg_h = own ? s->p.seg_rows
-                  : (int)std::max<int64_t>(2 * E, ceil_div(strip_rows, (int64_t)per_cu * s->cus));
-    } else {
-      seg_h = own ? s->p.seg_rows
-                  : (int)std::max<int64_t>(nlh::fast_seg_min(E), ceil_div(strip_rows, 1024));
+    }
+    // halo bands run beside the interior kernel (enqueue_step); their segments
+    // are short -- about one band workgroup per CU -- so that bands, the
+    // exchange they feed and the next pass's bands fit inside one interior
+    // pass.  NLH_BAND_SEG overrides the height (diagnostics)
+    int seg_band = seg_h;
+    if (fast) {
+      int64_t band_rows = 0;
+      for (auto &it : bnd) band_rows += ceil_div(it.r.x1 - it.r.x0, sw) * (it.r.y1 - it.r.y0);
+      const int lo = std::min(seg_h, 2 * E);
+      seg_band = (int)std::min<int64_t>(seg_h, std::max<int64_t>(lo, ceil_div(band_rows, (int64_t)s->cus)));
+      if (const char *bsg = std::getenv("NLH_BAND_SEG"))
+        if (std::atoi(bsg) > 0) seg_band = std::atoi(bsg);
+    }
+    return {seg_h, seg_band};
+  };
+  std::map<int, std::pair<int, int>> seg_of;  // (virtual) rank -> (interior, band) heights
+  if (s->vranks) {
+    for (int v : s->mine) {
+      std::vector<Item> a, in, bd;
+      for (auto &it : all) {
+        if (s->blocks[it.blk].owner != v) continue;
+        a.push_back(it);
+        (it.r.interior ? in : bd).push_back(it);
+      }
+      if (!a.empty()) seg_of[v] = sizes(a, in, bd);
     }
   }
-  (pair ? s->sc.seg_pair : s->sc.seg_h) = seg_h;
-  // halo bands run beside the interior kernel (enqueue_step); their segments
-  // are short -- about one band workgroup per CU -- so that bands, the
-  // exchange they feed and the next pass's bands fit inside one interior
-  // pass.  NLH_BAND_SEG overrides the height (diagnostics)
-  int seg_band = seg_h;
-  if (fast) {
-    int64_t band_rows = 0;
-    for (auto &it : bnd) band_rows += ceil_div(it.r.x1 - it.r.x0, sw) * (it.r.y1 - it.r.y0);
-    const int lo = std::min(seg_h, 2 * E);
-    seg_band = (int)std::min<int64_t>(seg_h, std::max<int64_t>(lo, ceil_div(band_rows, (int64_t)s->cus)));
-    if (const char *bsg = std::getenv("NLH_BAND_SEG"))
-      if (std::atoi(bsg) > 0) seg_band = std::atoi(bsg);
-  }
+  const std::pair<int, int> seg_all = sizes(all, inter, bnd);
+  (pair ? s->sc.seg_pair : s->sc.seg_h) = seg_all.first;
   auto make = [&](const std::vector<Item> &items, int k, std::vector<nlh::RectList> &out) -> int {
     out.clear();
     int w = 0;
@@ -463,7 +483,8 @@ int build_rectlists(nlh_solver *s, int kind) {
       fill_rect_common(R, s->blocks[it.blk], k, s);
       R.x0 = it.r.x0; R.y0 = it.r.y0; R.x1 = it.r.x1; R.y1 = it.r.y1;
       if (fast) {
-        R.seg_rows = it.r.interior ? seg_h : seg_band;
+        const std::pair<int, int> &sg = s->vranks ? seg_of[own] : seg_all;
+        R.seg_rows = it.r.interior ? sg.first : sg.second;
         R.nstrip = (int)ceil_div(R.x1 - R.x0, sw);
         R.nseg = (int)ceil_div(R.y1 - R.y0, R.seg_rows);
       } else {
