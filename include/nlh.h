@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define NLH_ABI_VERSION 7
+#define NLH_ABI_VERSION 8
 
 enum nlh_status {
   NLH_OK = 0,
@@ -50,7 +50,10 @@ enum nlh_status {
   NLH_ERR_HIP = 2,         /* HIP runtime failure                        */
   NLH_ERR_RCCL = 3,        /* RCCL failure                               */
   NLH_ERR_STATE = 4,       /* call not valid in the current state        */
-  NLH_ERR_UNSUPPORTED = 5  /* configuration not supported               */
+  NLH_ERR_UNSUPPORTED = 5, /* configuration not supported               */
+  NLH_ERR_NOMEM = 6        /* device memory too small for the request;
+                              the solver is unchanged (nlh_repartition /
+                              nlh_rebalance check before allocating)     */
 };
 
 /* Influence functions (nlh_params.influence) */

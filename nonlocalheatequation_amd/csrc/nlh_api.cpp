@@ -1118,6 +1118,50 @@ bool runs(const nlh_solver *s, int rank) {
   return std::find(s->mine.begin(), s->mine.end(), rank) != s->mine.end();
 }
 
+// The new solver is built beside the old one (both live until the tiles have
+// moved), plus one staging copy of the moving tiles on each side: check the
+// device's free memory against that before allocating anything, so a
+// rebalance that does not fit leaves the run as it was (NLH_ERR_NOMEM; the
+// distributed driver then skips that rebalance).  Every rank of a real
+// multi-rank run takes the same decision (minimum over ranks), so no rank
+// waits in a tile send that the others skip.
+int repartition_fits(nlh_solver *s, const std::vector<int32_t> &own) {
+  int64_t tiles_old = 0, tiles_new = 0, moving = 0;
+  for (size_t i = 0; i < own.size(); ++i) {
+    const bool ro = runs(s, s->owner[i]), rn = runs(s, own[i]);
+    tiles_old += ro;
+    tiles_new += rn;
+    if (own[i] != s->owner[i]) moving += (int64_t)ro + (int64_t)rn;
+  }
+  const int64_t tile_bytes = (s->p.nx / s->p.tiles_x) * (s->p.ny / s->p.tiles_y) * (int64_t)sizeof(double);
+  const double scale = tiles_old > 0 ? (double)tiles_new / (double)tiles_old : 1.0;
+  const double need = (double)s->device_bytes * scale * 1.05 + (double)(moving * tile_bytes) + 64.0 * (1 << 20);
+  size_t free_b = 0, total_b = 0;
+  HIP_TRY(hipMemGetInfo(&free_b, &total_b));
+  int32_t ok = (double)free_b >= need ? 1 : 0;
+  if (s->comm && !s->vranks && s->p.nranks > 1) {
+    int32_t *d = nullptr;
+    HIP_TRY(hipMalloc(&d, sizeof(int32_t)));
+    int st = NLH_OK;
+    if (hipMemcpyAsync(d, &ok, sizeof(int32_t), hipMemcpyHostToDevice, s->s_comm) != hipSuccess)
+      st = fail(NLH_ERR_HIP, "repartition memory check upload");
+    if (st == NLH_OK && ncclAllReduce(d, d, 1, ncclInt32, ncclMin, s->comm, s->s_comm) != ncclSuccess)
+      st = fail(NLH_ERR_RCCL, "repartition memory check all-reduce");
+    if (st == NLH_OK && hipMemcpyAsync(&ok, d, sizeof(int32_t), hipMemcpyDeviceToHost, s->s_comm) != hipSuccess)
+      st = fail(NLH_ERR_HIP, "repartition memory check download");
+    if (hipStreamSynchronize(s->s_comm) != hipSuccess && st == NLH_OK) st = fail(NLH_ERR_HIP, "repartition sync");
+    (void)hipFree(d);
+    if (st) return st;
+  }
+  if (!ok) {
+    char buf[200];
+    std::snprintf(buf, sizeof buf, "repartition needs ~%.0f MiB of device memory, %.0f MiB free (on this or another rank); "
+                  "the solver is unchanged", need / (1 << 20), (double)free_b / (1 << 20));
+    return fail(NLH_ERR_NOMEM, buf);
+  }
+  return NLH_OK;
+}
+
 // rebuild the solver for a new tile -> owner map, moving the tiles that
 // change rank over RCCL (src/2d_nonlocal_distributed.cpp:937-944).  Per
 // (virtual) rank pair A -> B the moving tiles travel in tile order as one
@@ -1134,6 +1178,7 @@ int repartition_impl(nlh_solver *s, const std::vector<int32_t> &own) {
   nlh_params p = s->p;
   p.owner = own.data();
   p.comm_id = nullptr;
+  if ((rc = repartition_fits(s, own))) return rc;
   nlh_solver *n = new nlh_solver();
   rc = create_impl(&p, n, s->comm);
   if (rc) {

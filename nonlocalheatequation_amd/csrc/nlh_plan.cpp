@@ -275,17 +275,31 @@ int balance_owner(int64_t tiles_x, int64_t tiles_y, int32_t nranks,
       for (int r = 0; r < nranks; ++r)
         if (w[r] > 0 && (br < 0 || w[r] > w[br])) br = r;
       if (bd < 0 || br < 0 || !(P[br] + tp[br] < P[bd])) break;
+      // distance of every tile to the receiver's nearest tile: one
+      // multi-source BFS over the tile grid (= the Manhattan distance, the grid
+      // has no obstacles), O(T) per move instead of donor x receiver pairs
+      std::vector<int64_t> dist((size_t)T, -1), queue;
+      queue.reserve((size_t)T);
+      for (int64_t t = 0; t < T; ++t)
+        if (o[t] == br) {
+          dist[t] = 0;
+          queue.push_back(t);
+        }
+      for (size_t h = 0; h < queue.size(); ++h) {
+        int64_t nb[4];
+        const int k = nbrs(queue[h], nb);
+        for (int j = 0; j < k; ++j)
+          if (dist[nb[j]] < 0) {
+            dist[nb[j]] = dist[queue[h]] + 1;
+            queue.push_back(nb[j]);
+          }
+      }
       int64_t bdist = -1;
       for (int64_t t = 0; t < T; ++t) {
         if (o[t] != bd) continue;
-        int64_t dist = n[br] ? -1 : 0;
-        for (int64_t u = 0; u < T && n[br]; ++u) {
-          if (o[u] != br) continue;
-          const int64_t dd = std::llabs(t % tiles_x - u % tiles_x) + std::llabs(t / tiles_x - u / tiles_x);
-          if (dist < 0 || dd < dist) dist = dd;
-        }
-        if (bdist < 0 || dist < bdist) {
-          bdist = dist;
+        const int64_t dt = n[br] ? dist[t] : 0;  // a receiver without tiles: any donor tile
+        if (bdist < 0 || dt < bdist) {
+          bdist = dt;
           bt = t;
         }
       }

@@ -114,8 +114,15 @@ __device__ __forceinline__ double wave_prefix_sum(double x) {
 // and the scan of row i+PA (its DPP chain and LDS write) is independent of
 // row i's window sums, so the two interleave instead of serialising each row
 // on scan -> LDS write -> LDS read.  Same arithmetic: bitwise equal to PA = 0.
+//
+// ILS (with PA, E <= 32): the scan reads and writes 64 full lanes of a padded
+// prefix slot without exec-mask branches (lanes past the staged row read
+// bytes no level ever uses) and without compiler barriers around it, so the
+// row's window reads, the scan of row i + PA and the row's taps form one
+// basic block and the scan's dependent DPP/add chain interleaves with the
+// taps instead of running alone.  Same arithmetic: bitwise equal.
 template <int E, int CH, bool TEST, int D = kWideD, int ABL = 0, int PIN = 1, bool AB = false, int OBP = 16,
-          bool SPLIT8 = true, bool PS = false, int PA = 0, bool PSPLIT = false>
+          bool SPLIT8 = true, bool PS = false, int PA = 0, bool PSPLIT = false, bool ILS = false>
 __global__ __launch_bounds__(64, 1) void k_wide(RectList L, StepConst C) {
   constexpr int W = 64;                 // output columns per strip
   constexpr int EP = (E + 1) & ~1;      // staged halo columns per side (16-B rows)
@@ -138,7 +145,8 @@ __global__ __launch_bounds__(64, 1) void k_wide(RectList L, StepConst C) {
   static_assert(!PS || (RW <= 256 && !AB), "prefix-sum rows: at most four staged doubles per lane");
   static_assert(PA == 0 || (PS && PA < D), "prefix-ahead rows need prefix sums and landed rows");
   constexpr int PK = PA ? pow2_ceil(PA + 1) : 1;  // prefix-row slots
-  constexpr int NPR = RW + 2;                      // doubles per prefix slot (16-B multiple)
+  static_assert(!ILS || (PA > 0 && RW <= 128), "interleaved scan: one 16-byte chunk per lane");
+  constexpr int NPR = ILS ? 130 : RW + 2;          // doubles per prefix slot (16-B multiple)
   constexpr int NP = PS ? PK * NPR : 0;  // prefix row: pfx[1] = 0, pfx[2 + k] = P(k)
   __shared__ __attribute__((aligned(16))) double ring[K * RWS + (TEST ? K * W + 2 * K : 0) + NP];
   double *lwr = ring + K * RWS;  // L_h[W0] rows (TEST), same slots as the u rows
@@ -212,6 +220,12 @@ __global__ __launch_bounds__(64, 1) void k_wide(RectList L, StepConst C) {
   auto scan_row = [&](int r) __attribute__((always_inline)) {
     const double *srow = ring + (r & (K - 1)) * RWS;
     double *dst = pfx + (r & (PK - 1)) * NPR + 2;
+    if constexpr (ILS) {
+      const double2 ab = *reinterpret_cast<const double2 *>(srow + 2 * lane);
+      const double sv = wave_prefix_sum(ab.x + ab.y);
+      *reinterpret_cast<double2 *>(dst + 2 * lane) = make_double2(sv - ab.y, sv);
+      return;
+    }
     double2 ab = make_double2(0.0, 0.0);
     if (2 * lane < RW) ab = *reinterpret_cast<const double2 *>(srow + 2 * lane);
     double2 cd = make_double2(0.0, 0.0);  // second chunk of the lane (E > 32)
@@ -342,7 +356,7 @@ __global__ __launch_bounds__(64, 1) void k_wide(RectList L, StepConst C) {
             if constexpr (PSPLIT) asm volatile("" ::: "memory");
           }
         });
-        asm volatile("" ::: "memory");  // the reads above are issued before the scan's write
+        if constexpr (!ILS) asm volatile("" ::: "memory");  // the reads above are issued before the scan's write
         scan_row(i + PA);
         acc[c + 2 * E] = wc;
         acc[c] += wc;
@@ -510,11 +524,16 @@ template <int E>
 constexpr int wide_pa() { return E <= 32 ? 2 : 0; }
 template <int E>
 constexpr int wide_chunk_pa() { return E <= 32 ? 8 : wide_chunk<E>(); }
+// ... with the scan interleaved into the taps (ILS): C4 153.4-155.6 ->
+// 156.9-157.6 G node/s in tools/wide_bench.hip, bitwise equal
+// (profiles/r03/wide_ils.jsonl)
+template <int E>
+constexpr bool wide_ils() { return wide_pa<E>() > 0; }
 
 template <int E, bool TEST>
 int launch_wide_e(const RectList &rl, const StepConst &c, hipStream_t st) {
   hipLaunchKernelGGL((k_wide<E, wide_chunk_pa<E>(), TEST, kWideD, 0, 1, false, 16, true, wide_ps<E>(), wide_pa<E>(),
-                             (wide_pa<E>() > 0)>),
+                             (wide_pa<E>() > 0), wide_ils<E>()>),
                      dim3(rl.nwork), dim3(64), 0, st, rl, c);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : (int)e;
@@ -527,7 +546,7 @@ int wide_blocks_per_cu_e() {
   int n = 0;
   const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
       &n, k_wide<E, wide_chunk_pa<E>(), false, kWideD, 0, 1, false, 16, true, wide_ps<E>(), wide_pa<E>(),
-             (wide_pa<E>() > 0)>,
+             (wide_pa<E>() > 0), wide_ils<E>()>,
       64, 0);
   return e == hipSuccess ? n : 0;
 }

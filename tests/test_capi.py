@@ -37,7 +37,7 @@ def test_python_binding_covers_header():
 
 
 def test_abi_version():
-    assert N.lib().nlh_abi_version() == 7
+    assert N.lib().nlh_abi_version() == 8
 
 
 def test_build_id_matches_sources():

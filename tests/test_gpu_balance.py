@@ -242,3 +242,54 @@ def test_driver_runs_partitioner_file(oracle, tmp_path):
     l2, li = oracle.errors(pp, nt, oracle.run(pp, nt))
     m = re.search(r"^l2: (\S+) linfinity: (\S+)$", out.stdout, re.M)
     assert m and float(m.group(1)) == pytest.approx(l2, rel=1e-5) and float(m.group(2)) == pytest.approx(li, rel=1e-5)
+
+
+def test_repartition_without_memory_leaves_solver_unchanged(oracle, monkeypatch):
+    """A repartition needs the new solver beside the old one: with too little
+    free device memory nlh_repartition fails with NLH_ERR_NOMEM (status 6)
+    before allocating or sending anything, the field and step index stay as
+    they were, and the run continues (bitwise vs the oracle, exact kernel);
+    with the memory back the same repartition goes through."""
+    import ctypes
+    monkeypatch.setenv("NLH_VIRTUAL_RANKS", "2")
+    hip = ctypes.CDLL("/opt/rocm/lib/libamdhip64.so")
+    nx, ny, eps, tiles = 2048, 2048, 4, (4, 4)
+    dh = 1.0 / nx
+    dt = eps ** 4 * dh * dh / (8 * N.disk_count(eps))
+    p = oracle.params(nx, ny, eps, 1.0, dt, dh, 1)
+    own0 = np.repeat(np.arange(2, dtype=np.int32), 8)
+    own1 = own0[::-1].copy()
+    held = []
+
+    def free_bytes():
+        f, t = ctypes.c_size_t(), ctypes.c_size_t()
+        assert hip.hipMemGetInfo(ctypes.byref(f), ctypes.byref(t)) == 0
+        return f.value
+
+    with N.Solver(nx, ny, eps, 1.0, dt, dh, kernel="exact", test=True, tiles=tiles, owner=own0) as s:
+        s.test_init()
+        s.run(2)
+        s.synchronize()
+        before = s.field()
+        try:
+            target = 96 << 20  # leave less than the new solver needs (~2 x 35 MB + 64 MiB margin)
+            chunk = 16 << 30
+            while free_bytes() > target + (8 << 20) and chunk >= (1 << 20):
+                ptr = ctypes.c_void_p()
+                size = min(chunk, free_bytes() - target)
+                if hip.hipMalloc(ctypes.byref(ptr), ctypes.c_size_t(size)) == 0:
+                    held.append(ptr)
+                else:
+                    chunk //= 2
+            with pytest.raises(N.NLHError, match=r"status 6"):
+                s.repartition(own1)
+        finally:
+            for ptr in held:
+                hip.hipFree(ptr)
+        assert s.step_index == 2
+        assert np.array_equal(s.field(), before)
+        s.run(1)
+        s.repartition(own1)
+        s.run(2)
+        s.synchronize()
+        _check(oracle, s.field(), p, 5, "exact")

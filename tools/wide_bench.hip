@@ -76,20 +76,16 @@ int main(int argc, char **argv) {
   // variants: prefix-sum rows (production, PA = 0) and prefix rows built PA
   // rows ahead (k_wide PA), at DMA depths 6 and 8
   std::vector<Variant> vs = {
-      {"wide_ps_C12_D6", k_wide<E, 12, false, 6, 0, 1, false, 16, true, true>, 64, 8},
-      {"wide_ps_split_C12_D6_PA0", k_wide<E, 12, false, 6, 0, 1, false, 16, true, true, 0, true>, 64, 8},
-      {"wide_ps_split_C12_D6_PA2", k_wide<E, 12, false, 6, 0, 1, false, 16, true, true, 2, true>, 64, 8},
-      {"wide_ps_split_C12_D6_PA1", k_wide<E, 12, false, 6, 0, 1, false, 16, true, true, 1, true>, 64, 8},
-      {"wide_ps_split_C12_D8_PA2", k_wide<E, 12, false, 8, 0, 1, false, 16, true, true, 2, true>, 64, 8},
-      {"wide_ps_split_C12_D8_PA3", k_wide<E, 12, false, 8, 0, 1, false, 16, true, true, 3, true>, 64, 8},
-      {"wide_ps_split_C8_D6_PA2", k_wide<E, 8, false, 6, 0, 1, false, 16, true, true, 2, true>, 64, 8},
-      {"wide_ps_split_C8_D8_PA2", k_wide<E, 8, false, 8, 0, 1, false, 16, true, true, 2, true>, 64, 8},
-      {"wide_ps_split_C8_D6_PA3", k_wide<E, 8, false, 6, 0, 1, false, 16, true, true, 3, true>, 64, 8},
-      {"wide_ps_split_C8_D8_PA4", k_wide<E, 8, false, 8, 0, 1, false, 16, true, true, 4, true>, 64, 8},
-      {"wide_ps_split_C16_D6_PA2", k_wide<E, 16, false, 6, 0, 1, false, 16, true, true, 2, true>, 64, 8},
-      {"wide_ps_split_C10_D6_PA2", k_wide<E, 10, false, 6, 0, 1, false, 16, true, true, 2, true>, 64, 8},
-      {"wide_ps_split_C6_D6_PA2", k_wide<E, 6, false, 6, 0, 1, false, 16, true, true, 2, true>, 64, 8},
+      {"prod_C8_D6_PA2", k_wide<E, 8, false, 6, 0, 1, false, 16, true, true, 2, true>, 64, 8},
+      {"ils_C8_D6_PA2", k_wide<E, 8, false, 6, 0, 1, false, 16, true, true, 2, true, true>, 64, 8},
+      {"ils_C8_D6_PA1", k_wide<E, 8, false, 6, 0, 1, false, 16, true, true, 1, true, true>, 64, 8},
+      {"ils_C8_D6_PA3", k_wide<E, 8, false, 6, 0, 1, false, 16, true, true, 3, true, true>, 64, 8},
+      {"ils_C12_D6_PA2", k_wide<E, 12, false, 6, 0, 1, false, 16, true, true, 2, true, true>, 64, 8},
+      {"ils_C8_D8_PA2", k_wide<E, 8, false, 8, 0, 1, false, 16, true, true, 2, true, true>, 64, 8},
+      {"prod_C8_D6_PA2_again", k_wide<E, 8, false, 6, 0, 1, false, 16, true, true, 2, true>, 64, 8},
+      {"ils_C8_D6_PA2_again", k_wide<E, 8, false, 6, 0, 1, false, 16, true, true, 2, true, true>, 64, 8},
   };
+
   std::vector<double> ref((size_t)n * n), got((size_t)n * n);
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
