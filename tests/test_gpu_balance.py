@@ -252,7 +252,13 @@ def test_repartition_without_memory_leaves_solver_unchanged(oracle, monkeypatch)
     with the memory back the same repartition goes through."""
     import ctypes
     monkeypatch.setenv("NLH_VIRTUAL_RANKS", "2")
-    hip = ctypes.CDLL("/opt/rocm/lib/libamdhip64.so")
+    N.lib()
+    # the HIP runtime libnlh runs on (the copy already mapped in this process:
+    # loading a second one by path would clash with the loaded HSA runtime)
+    with open("/proc/self/maps") as f:
+        paths = sorted({ln.split()[-1] for ln in f if "libamdhip64.so" in ln})
+    assert paths, "no HIP runtime mapped"
+    hip = ctypes.CDLL(paths[0])
     nx, ny, eps, tiles = 2048, 2048, 4, (4, 4)
     dh = 1.0 / nx
     dt = eps ** 4 * dh * dh / (8 * N.disk_count(eps))

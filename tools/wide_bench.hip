@@ -78,13 +78,13 @@ int main(int argc, char **argv) {
   std::vector<Variant> vs = {
       {"prod_C8_D6_PA2", k_wide<E, 8, false, 6, 0, 1, false, 16, true, true, 2, true>, 64, 8},
       {"ils_C8_D6_PA2", k_wide<E, 8, false, 6, 0, 1, false, 16, true, true, 2, true, true>, 64, 8},
-      {"ils_C8_D6_PA1", k_wide<E, 8, false, 6, 0, 1, false, 16, true, true, 1, true, true>, 64, 8},
-      {"ils_C8_D6_PA3", k_wide<E, 8, false, 6, 0, 1, false, 16, true, true, 3, true, true>, 64, 8},
-      {"ils_C12_D6_PA2", k_wide<E, 12, false, 6, 0, 1, false, 16, true, true, 2, true, true>, 64, 8},
-      {"ils_C8_D8_PA2", k_wide<E, 8, false, 8, 0, 1, false, 16, true, true, 2, true, true>, 64, 8},
       {"prod_C8_D6_PA2_again", k_wide<E, 8, false, 6, 0, 1, false, 16, true, true, 2, true>, 64, 8},
       {"ils_C8_D6_PA2_again", k_wide<E, 8, false, 6, 0, 1, false, 16, true, true, 2, true, true>, 64, 8},
   };
+
+
+
+
 
   std::vector<double> ref((size_t)n * n), got((size_t)n * n);
   hipEvent_t e0, e1;
