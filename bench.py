@@ -157,7 +157,7 @@ def live_pmc(args, wkey: str):
     env = dict(os.environ, NLH_N=str(args.lattice), NLH_EPS=str(args.eps), NLH_TEST=str(int(args.test_mode)),
                NLH_KERNEL=args.kernel, NLH_INFLUENCE=args.influence, NLH_SEG=str(args.seg_rows),
                TMPDIR="/tmp")
-    vals, durs, seen = {}, [], set()
+    vals, durs, seen = {}, {}, set()
     with tempfile.TemporaryDirectory(dir="/tmp") as td:
         for i, grp in enumerate(PMC_PASSES):
             out = os.path.join(td, f"p{i}")
@@ -181,12 +181,17 @@ def live_pmc(args, wkey: str):
                     if fn.endswith("counter_collection.csv"):
                         for row in csv.DictReader(open(path)):
                             if key in row["Kernel_Name"]:
-                                vals.setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
+                                vals.setdefault(row["Counter_Name"], {}).setdefault(
+                                    row["Kernel_Name"], []).append(float(row["Counter_Value"]))
                     elif fn.endswith("kernel_trace.csv"):
                         for row in csv.DictReader(open(path)):
                             if key in row["Kernel_Name"]:
-                                durs.append(int(row["End_Timestamp"]) - int(row["Start_Timestamp"]))
-    med = {k: statistics.median(v) for k, v in vals.items()}
+                                durs.setdefault(row["Kernel_Name"], []).append(
+                                    int(row["End_Timestamp"]) - int(row["Start_Timestamp"]))
+    # per pass: the median of each kernel instance, summed over the instances a
+    # pass launches (k_wide_rt: its two half-disk launches; otherwise one)
+    med = {c: sum(statistics.median(v) for v in per.values()) for c, per in vals.items()}
+    durs = [sum(statistics.median(v) for v in durs.values())] if durs else []
     if len(seen) != 1 or not {"FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU"} <= set(med):
         return None
     node_updates = nodes * spp
@@ -472,6 +477,9 @@ def main() -> int:
                 "traffic": traffic,
                 "achieved_is": "effective (algorithmic bytes / launch time)",
                 "kernel": kname,
+                # k_wide_rt splits a step's disk over two launches: its "launch"
+                # figures here are per step (both launches together)
+                "launches_per_pass": 2 if kname == "k_wide_rt" else 1,
                 "steps_per_launch": spp,
                 "kernel_avg_us": avg_launch_s * 1e6,
                 "kernel_launches_timed": passes,

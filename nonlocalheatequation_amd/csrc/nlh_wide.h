@@ -122,7 +122,7 @@ __device__ __forceinline__ double wave_prefix_sum(double x) {
 // basic block and the scan's dependent DPP/add chain interleaves with the
 // taps instead of running alone.  Same arithmetic: bitwise equal.
 template <int E, int CH, bool TEST, int D = kWideD, int ABL = 0, int PIN = 1, bool AB = false, int OBP = 16,
-          bool SPLIT8 = true, bool PS = false, int PA = 0, bool PSPLIT = false, bool ILS = false>
+          bool SPLIT8 = true, bool PS = false, int PA = 0, bool PSPLIT = false, bool ILS = false, bool NTS = false>
 __global__ __launch_bounds__(64, 1) void k_wide(RectList L, StepConst C) {
   constexpr int W = 64;                 // output columns per strip
   constexpr int EP = (E + 1) & ~1;      // staged halo columns per side (16-B rows)
@@ -490,7 +490,13 @@ __global__ __launch_bounds__(64, 1) void k_wide(RectList L, StepConst C) {
       constexpr int a = decltype(ac)::value;
       const int k = ibase - 2 * E + a;
       if (k < 0 || k >= nout) return;
-      if (emit) run[(int64_t)(up ? Y1 - 1 - k : Y0 + k) * pitch + xl] = alpha * acc[a];
+      if (emit) {
+        double *dst = run + (int64_t)(up ? Y1 - 1 - k : Y0 + k) * pitch + xl;
+        if constexpr (NTS)
+          __builtin_nontemporal_store(alpha * acc[a], dst);  // NTS: streaming store (tools/ harness)
+        else
+          *dst = alpha * acc[a];
+      }
     };
     static_for<CH>(store);
     // rename: a -> a - CH
@@ -526,14 +532,15 @@ template <int E>
 constexpr int wide_chunk_pa() { return E <= 32 ? 8 : wide_chunk<E>(); }
 // ... with the scan interleaved into the taps (ILS): C4 153.4-155.6 ->
 // 156.9-157.6 G node/s in tools/wide_bench.hip, bitwise equal
-// (profiles/r03/wide_ils.jsonl)
+// (profiles/r03/wide_ils.jsonl); and non-temporal output stores (NTS, the
+// same instances): +1-2% (profiles/r03/wide_nts.jsonl)
 template <int E>
 constexpr bool wide_ils() { return wide_pa<E>() > 0; }
 
 template <int E, bool TEST>
 int launch_wide_e(const RectList &rl, const StepConst &c, hipStream_t st) {
   hipLaunchKernelGGL((k_wide<E, wide_chunk_pa<E>(), TEST, kWideD, 0, 1, false, 16, true, wide_ps<E>(), wide_pa<E>(),
-                             (wide_pa<E>() > 0), wide_ils<E>()>),
+                             (wide_pa<E>() > 0), wide_ils<E>(), wide_ils<E>()>),
                      dim3(rl.nwork), dim3(64), 0, st, rl, c);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : (int)e;
@@ -546,7 +553,7 @@ int wide_blocks_per_cu_e() {
   int n = 0;
   const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
       &n, k_wide<E, wide_chunk_pa<E>(), false, kWideD, 0, 1, false, 16, true, wide_ps<E>(), wide_pa<E>(),
-             (wide_pa<E>() > 0), wide_ils<E>()>,
+             (wide_pa<E>() > 0), wide_ils<E>(), wide_ils<E>()>,
       64, 0);
   return e == hipSuccess ? n : 0;
 }

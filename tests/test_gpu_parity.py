@@ -153,7 +153,7 @@ def test_large_eps_runtime_horizon(oracle, eps, test):
     p = oracle.params(nx, ny, eps, r.k, r.dt, dh, int(test))
     ref = oracle.run(p, nt, u0)
     u, (l2, _), info = _gpu_run_j(r, test, "auto", "constant", u0)
-    assert info.pass_kernel == "k_wide" and info.kernel == N.KERNEL_FAST
+    assert info.pass_kernel == "k_wide_rt" and info.kernel == N.KERNEL_FAST
     d = np.max(np.abs(u - ref))
     scale = np.max(np.abs(ref))
     assert d <= 1e-12 * scale, d
@@ -190,7 +190,7 @@ def test_large_eps_runtime_horizon_blocks(oracle, monkeypatch, eps, tiles):
         s.run(nt)
         s.synchronize()
         u = s.field()
-        assert s.info().pass_kernel == "k_wide"
+        assert s.info().pass_kernel == "k_wide_rt"
     assert np.max(np.abs(u - ref)) <= 1e-12 * np.max(np.abs(ref))
 
 

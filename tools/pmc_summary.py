@@ -33,18 +33,23 @@ def main():
     ap.add_argument("--build-id", default=None)
     a = ap.parse_args()
     key = a.kernel + "<"
-    vals, durs = {}, []
+    vals, kdurs = {}, {}
     for f in sorted(glob.glob(os.path.join(a.dir, "p*", "run_counter_collection.csv"))):
         for row in csv.DictReader(open(f)):
             if key in row["Kernel_Name"]:
-                vals.setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
+                vals.setdefault(row["Counter_Name"], {}).setdefault(row["Kernel_Name"], []).append(
+                    float(row["Counter_Value"]))
     for f in sorted(glob.glob(os.path.join(a.dir, "p*", "run_kernel_trace.csv"))):
         for row in csv.DictReader(open(f)):
             if key in row["Kernel_Name"]:
-                durs.append(int(row["End_Timestamp"]) - int(row["Start_Timestamp"]))
-    med = {k: statistics.median(v) for k, v in vals.items()}
+                kdurs.setdefault(row["Kernel_Name"], []).append(int(row["End_Timestamp"]) - int(row["Start_Timestamp"]))
+    # a "launch" here is one pass: the median of each kernel instance, summed
+    # over the instances the pass launches (k_wide_rt: two half-disk launches)
+    med = {c: sum(statistics.median(v) for v in per.values()) for c, per in vals.items()}
+    durs = [sum(statistics.median(v) for v in kdurs.values())] if kdurs else []
     out = {"kernel_match": a.kernel, "workload": a.workload, "commit": a.commit, "build_id": a.build_id,
-           "dispatches_per_counter": {k: len(v) for k, v in vals.items()}, "median": med}
+           "dispatches_per_counter": {c: sum(len(v) for v in per.values()) for c, per in vals.items()},
+           "kernel_instances_per_pass": len(kdurs), "median": med}
     if "FETCH_SIZE" in med and "WRITE_SIZE" in med:
         rd = 2.0 * med["FETCH_SIZE"] * 1024
         wr = med["WRITE_SIZE"] * 1024

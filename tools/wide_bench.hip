@@ -76,11 +76,12 @@ int main(int argc, char **argv) {
   // variants: prefix-sum rows (production, PA = 0) and prefix rows built PA
   // rows ahead (k_wide PA), at DMA depths 6 and 8
   std::vector<Variant> vs = {
-      {"prod_C8_D6_PA2", k_wide<E, 8, false, 6, 0, 1, false, 16, true, true, 2, true>, 64, 8},
       {"ils_C8_D6_PA2", k_wide<E, 8, false, 6, 0, 1, false, 16, true, true, 2, true, true>, 64, 8},
-      {"prod_C8_D6_PA2_again", k_wide<E, 8, false, 6, 0, 1, false, 16, true, true, 2, true>, 64, 8},
-      {"ils_C8_D6_PA2_again", k_wide<E, 8, false, 6, 0, 1, false, 16, true, true, 2, true, true>, 64, 8},
+      {"ils_nts", k_wide<E, 8, false, 6, 0, 1, false, 16, true, true, 2, true, true, true>, 64, 8},
+      {"ils_again", k_wide<E, 8, false, 6, 0, 1, false, 16, true, true, 2, true, true>, 64, 8},
+      {"ils_nts_again", k_wide<E, 8, false, 6, 0, 1, false, 16, true, true, 2, true, true, true>, 64, 8},
   };
+
 
 
 
