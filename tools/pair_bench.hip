@@ -84,16 +84,14 @@ int main(int argc, char **argv) {
   // only (no LDS reads, no vmcnt waits, no stores, no DMA)
   std::vector<Variant> vs = {
       {"split_D8_B4", k_pair_split<E, 8, 0, 4>, 128, 4, 128 - 2 * E},
-      {"abl_no_dma_no_store", k_pair_split<E, 8, 384, 4>, 128, 4, 128 - 2 * E},
+      {"abl8_no_barrier", k_pair_split<E, 8, 8, 4>, 128, 4, 128 - 2 * E},
       {"abl_valu_only", k_pair_split<E, 8, 452, 4>, 128, 4, 128 - 2 * E},
-      {"split_D8_B2", k_pair_split<E, 8, 0, 2>, 128, 4, 128 - 2 * E},
-      {"split_D6_B4", k_pair_split<E, 6, 0, 4>, 128, 4, 128 - 2 * E},
-      {"split_D4_B4", k_pair_split<E, 4, 0, 4>, 128, 4, 128 - 2 * E},
-      {"split_D4_B2", k_pair_split<E, 4, 0, 2>, 128, 4, 128 - 2 * E},
-      {"split_D4_B2_6wg", k_pair_split<E, 4, 0, 2>, 128, 6, 128 - 2 * E},
-      {"split_D8_B4_seg76", k_pair_split<E, 8, 0, 4>, 128, 8, 128 - 2 * E},
-      {"split_D8_B4_seg304", k_pair_split<E, 8, 0, 4>, 128, 2, 128 - 2 * E},
+      {"abl_valu_only_no_barrier", k_pair_split<E, 8, 460, 4>, 128, 4, 128 - 2 * E},
+      {"abl8_no_barrier_B8", k_pair_split<E, 8, 8, 8>, 128, 4, 128 - 2 * E},
+      {"split_D8_B8", k_pair_split<E, 8, 0, 8>, 128, 4, 128 - 2 * E},
   };
+
+
 
   std::vector<double> ref((size_t)n * n), got((size_t)n * n);
   hipEvent_t e0, e1;
