@@ -24,7 +24,7 @@ HOSTFLAGS := -O2 $(CXXSTD) -fPIC $(WARN) $(INC) -D__HIP_PLATFORM_AMD__ -I$(ROCM)
 BUILD_ID_SRCS := $(sort $(wildcard $(CSRC)/*.hip $(CSRC)/*.h $(CSRC)/*.cpp) include/nlh.h Makefile)
 BUILD_ID := $(shell cat $(BUILD_ID_SRCS) | sha256sum | cut -c1-16)
 
-FAST_UNITS := $(sort $(wildcard $(CSRC)/nlh_fast_e*.hip $(CSRC)/nlh_pair_e*.hip $(CSRC)/nlh_wide_e*.hip) $(CSRC)/nlh_wide_rt.hip)
+FAST_UNITS := $(sort $(wildcard $(CSRC)/nlh_fast_e*.hip $(CSRC)/nlh_pair_e*.hip $(CSRC)/nlh_wide_e*.hip))
 FAST_OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(FAST_UNITS))
 LIB_OBJS := $(OBJDIR)/nlh_kernels.o $(FAST_OBJS) $(OBJDIR)/nlh_api.o $(OBJDIR)/nlh_plan.o $(OBJDIR)/nlh_1d.o
 # the fast kernel is fully unrolled over 2E+1 rows; lift LLVM's pragma-unroll
@@ -56,9 +56,6 @@ $(OBJDIR)/nlh_pair_%.o: $(CSRC)/nlh_pair_%.hip $(CHDRS) $(CSRC)/nlh_pair.h | $(O
 	$(HIPCC) $(HIPFLAGS) $(UNROLL) -c $< -o $@
 
 $(OBJDIR)/nlh_wide_%.o: $(CSRC)/nlh_wide_%.hip $(CHDRS) $(CSRC)/nlh_wide.h | $(OBJDIR)
-	$(HIPCC) $(HIPFLAGS) $(UNROLL) -c $< -o $@
-
-$(OBJDIR)/nlh_wide_rt.o: $(CSRC)/nlh_wide_rt.hip $(CHDRS) $(CSRC)/nlh_wide.h $(CSRC)/nlh_wide_rt.h | $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) $(UNROLL) -c $< -o $@
 
 $(OBJDIR)/nlh_api.o: $(CSRC)/nlh_api.cpp $(BUILD_ID_SRCS) | $(OBJDIR)

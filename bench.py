@@ -189,7 +189,7 @@ def live_pmc(args, wkey: str):
                                 durs.setdefault(row["Kernel_Name"], []).append(
                                     int(row["End_Timestamp"]) - int(row["Start_Timestamp"]))
     # per pass: the median of each kernel instance, summed over the instances a
-    # pass launches (k_wide_rt: its two half-disk launches; otherwise one)
+    # pass launches (one for every kernel libnlh has today)
     med = {c: sum(statistics.median(v) for v in per.values()) for c, per in vals.items()}
     durs = [sum(statistics.median(v) for v in durs.values())] if durs else []
     if len(seen) != 1 or not {"FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU"} <= set(med):
@@ -477,9 +477,6 @@ def main() -> int:
                 "traffic": traffic,
                 "achieved_is": "effective (algorithmic bytes / launch time)",
                 "kernel": kname,
-                # k_wide_rt splits a step's disk over two launches: its "launch"
-                # figures here are per step (both launches together)
-                "launches_per_pass": 2 if kname == "k_wide_rt" else 1,
                 "steps_per_launch": spp,
                 "kernel_avg_us": avg_launch_s * 1e6,
                 "kernel_launches_timed": passes,

@@ -1662,7 +1662,7 @@ int nlh_get_info(const nlh_solver *s, nlh_info *info) {
   info->steps_per_pass = s->pair ? 2 : 1;
   info->owners = s->owners;
   const char *pk = s->pair ? "k_pair_split"
-                           : s->wide ? (s->p.eps > 48 ? "k_wide_rt" : "k_wide") : s->weighted ? "k_weighted"
+                           : s->wide ? "k_wide" : s->weighted ? "k_weighted"
                            : s->kernel == NLH_KERNEL_FAST ? "k_fast"
                            : nlh::exact_lds_ok((int)s->p.eps, s->p.test != 0) ? "k_exact_lds" : "k_exact";
   std::snprintf(info->pass_kernel, sizeof(info->pass_kernel), "%s", pk);

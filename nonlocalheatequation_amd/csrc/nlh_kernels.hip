@@ -536,23 +536,20 @@ NLH_WIDE_EXTERN(33) NLH_WIDE_EXTERN(34) NLH_WIDE_EXTERN(35) NLH_WIDE_EXTERN(36)
 NLH_WIDE_EXTERN(37) NLH_WIDE_EXTERN(38) NLH_WIDE_EXTERN(39) NLH_WIDE_EXTERN(40)
 NLH_WIDE_EXTERN(41) NLH_WIDE_EXTERN(42) NLH_WIDE_EXTERN(43) NLH_WIDE_EXTERN(44)
 NLH_WIDE_EXTERN(45) NLH_WIDE_EXTERN(46) NLH_WIDE_EXTERN(47) NLH_WIDE_EXTERN(48)
+NLH_WIDE_EXTERN(49) NLH_WIDE_EXTERN(50) NLH_WIDE_EXTERN(51) NLH_WIDE_EXTERN(52)
+NLH_WIDE_EXTERN(53) NLH_WIDE_EXTERN(54) NLH_WIDE_EXTERN(55) NLH_WIDE_EXTERN(56)
+NLH_WIDE_EXTERN(57) NLH_WIDE_EXTERN(58) NLH_WIDE_EXTERN(59) NLH_WIDE_EXTERN(60)
+NLH_WIDE_EXTERN(61) NLH_WIDE_EXTERN(62) NLH_WIDE_EXTERN(63) NLH_WIDE_EXTERN(64)
 
-// k_wide: compile-time instances for eps 17..48 (nlh_wide.h), the
-// run-time-horizon two-pass k_wide_rt for 49..64 (nlh_wide_rt.h)
+// k_wide: compile-time instances for eps 17..64 (nlh_wide.h)
 bool wide_supported(int E) { return E >= 17 && E <= 64; }
-
-template <bool TEST>
-int launch_wide_rt_t(const RectList &rl, const StepConst &c, hipStream_t st);
-extern template int launch_wide_rt_t<true>(const RectList &, const StepConst &, hipStream_t);
-extern template int launch_wide_rt_t<false>(const RectList &, const StepConst &, hipStream_t);
-int wide_rt_blocks_per_cu();
 
 #define NLH_WIDE_CASES(X)                                                                          \
   X(17) X(18) X(19) X(20) X(21) X(22) X(23) X(24) X(25) X(26) X(27) X(28) X(29) X(30) X(31) X(32) \
-  X(33) X(34) X(35) X(36) X(37) X(38) X(39) X(40) X(41) X(42) X(43) X(44) X(45) X(46) X(47) X(48)
+  X(33) X(34) X(35) X(36) X(37) X(38) X(39) X(40) X(41) X(42) X(43) X(44) X(45) X(46) X(47) X(48) \
+  X(49) X(50) X(51) X(52) X(53) X(54) X(55) X(56) X(57) X(58) X(59) X(60) X(61) X(62) X(63) X(64)
 
 int wide_blocks_per_cu(int E) {
-  if (E > 48) return wide_rt_blocks_per_cu();
   switch (E) {
 #define NLH_CASEWO(EE) \
   case EE:             \
@@ -566,7 +563,6 @@ int wide_blocks_per_cu(int E) {
 
 int launch_wide(const RectList &rl, const StepConst &c, bool test, void *stream) {
   hipStream_t st = (hipStream_t)stream;
-  if (c.E > 48 && c.E <= 64) return test ? launch_wide_rt_t<true>(rl, c, st) : launch_wide_rt_t<false>(rl, c, st);
   switch (c.E) {
 #define NLH_CASEW(EE) \
   case EE:            \

@@ -140,12 +140,12 @@ def test_eps32_golden(kernel, test):
 
 @pytest.mark.parametrize("eps", [49, 52, 53, 57, 64])
 @pytest.mark.parametrize("test", [False, True])
-def test_large_eps_runtime_horizon(oracle, eps, test):
-    """eps 49..64 (past the compile-time k_wide instances): AUTO/FAST run
-    k_wide_rt -- prefix-sum row windows at run-time offsets, the disk's row
-    offsets split over two passes; per node within 1e-12 of field scale (no
-    allowance), L2 as the oracle's; EXACT stays bitwise.  Ragged lattice
-    narrower than two strips, segments shorter than the horizon."""
+def test_large_eps_64(oracle, eps, test):
+    """eps 49..64: AUTO/FAST run k_wide's compile-time instances (nested
+    windows, 8-row chunks, accumulators partly in AGPRs); per node within
+    1e-12 of field scale (no allowance), L2 as the oracle's; EXACT stays
+    bitwise.  Ragged lattice narrower than two strips, segments shorter than
+    the horizon."""
     nx, ny, nt = 150, 133, 3
     dh = 1.0 / nx
     r = N.BatchRow(nx, ny, nt, eps, 1.0, 0.5 * eps ** 4 * dh * dh / (8 * N.disk_count(eps)), dh)
@@ -153,7 +153,7 @@ def test_large_eps_runtime_horizon(oracle, eps, test):
     p = oracle.params(nx, ny, eps, r.k, r.dt, dh, int(test))
     ref = oracle.run(p, nt, u0)
     u, (l2, _), info = _gpu_run_j(r, test, "auto", "constant", u0)
-    assert info.pass_kernel == "k_wide_rt" and info.kernel == N.KERNEL_FAST
+    assert info.pass_kernel == "k_wide" and info.kernel == N.KERNEL_FAST
     d = np.max(np.abs(u - ref))
     scale = np.max(np.abs(ref))
     assert d <= 1e-12 * scale, d
@@ -167,8 +167,8 @@ def test_large_eps_runtime_horizon(oracle, eps, test):
 
 @pytest.mark.parametrize("eps", [56, 64])
 @pytest.mark.parametrize("tiles", [(1, 1), (3, 2)])
-def test_large_eps_runtime_horizon_blocks(oracle, monkeypatch, eps, tiles):
-    """k_wide_rt through the multi-block exchange (RCCL to self) and over
+def test_large_eps_64_blocks(oracle, monkeypatch, eps, tiles):
+    """k_wide at eps 56 / 64 through the multi-block exchange (RCCL to self) and over
     several segments per strip, production mode, vs the oracle.  The IC is
     smooth plus 1e-2 noise: a field of pure noise shrinks 30x in three steps
     at this horizon, and the reference order's own rounding (12,853 terms
@@ -190,7 +190,7 @@ def test_large_eps_runtime_horizon_blocks(oracle, monkeypatch, eps, tiles):
         s.run(nt)
         s.synchronize()
         u = s.field()
-        assert s.info().pass_kernel == "k_wide_rt"
+        assert s.info().pass_kernel == "k_wide"
     assert np.max(np.abs(u - ref)) <= 1e-12 * np.max(np.abs(ref))
 
 

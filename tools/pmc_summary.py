@@ -44,7 +44,7 @@ def main():
             if key in row["Kernel_Name"]:
                 kdurs.setdefault(row["Kernel_Name"], []).append(int(row["End_Timestamp"]) - int(row["Start_Timestamp"]))
     # a "launch" here is one pass: the median of each kernel instance, summed
-    # over the instances the pass launches (k_wide_rt: two half-disk launches)
+    # over the instances the pass launches (one for every kernel libnlh has today)
     med = {c: sum(statistics.median(v) for v in per.values()) for c, per in vals.items()}
     durs = [sum(statistics.median(v) for v in kdurs.values())] if kdurs else []
     out = {"kernel_match": a.kernel, "workload": a.workload, "commit": a.commit, "build_id": a.build_id,

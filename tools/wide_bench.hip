@@ -35,13 +35,16 @@ struct Variant {
   int wg_per_cu;  // resident workgroups per CU
 };
 
-constexpr int E = 32;
+#ifndef WB_E
+#define WB_E 32
+#endif
+constexpr int E = WB_E;  // -DWB_E=56: the compile-time instance of another horizon
 static int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 int main(int argc, char **argv) {
   const int n = argc > 1 ? std::atoi(argv[1]) : 8192;
   const int steps = argc > 2 ? std::atoi(argv[2]) : 20;
-  const int H = E, XL = 32;
+  const int H = E, XL = E > 32 ? (E + 7) / 8 * 8 : 32;  // staged rows start EP columns left of a strip
   const int64_t pitch = (XL + ceil_div(n, 256) * 256 + XL + 7) / 8 * 8;
   const int64_t rows = n + 2 * H;
   const size_t bytes = (size_t)(pitch * rows) * sizeof(double) + 256;
@@ -75,12 +78,22 @@ int main(int argc, char **argv) {
   const int cus = prop.multiProcessorCount;
   // variants: prefix-sum rows (production, PA = 0) and prefix rows built PA
   // rows ahead (k_wide PA), at DMA depths 6 and 8
+#if WB_E <= 32
   std::vector<Variant> vs = {
+      {"prod_C8_D6_PA2", k_wide<E, 8, false, 6, 0, 1, false, 16, true, true, 2, true>, 64, 8},
       {"ils_C8_D6_PA2", k_wide<E, 8, false, 6, 0, 1, false, 16, true, true, 2, true, true>, 64, 8},
       {"ils_nts", k_wide<E, 8, false, 6, 0, 1, false, 16, true, true, 2, true, true, true>, 64, 8},
-      {"ils_again", k_wide<E, 8, false, 6, 0, 1, false, 16, true, true, 2, true, true>, 64, 8},
-      {"ils_nts_again", k_wide<E, 8, false, 6, 0, 1, false, 16, true, true, 2, true, true, true>, 64, 8},
   };
+#else
+  // nested windows, 8-row chunks (the production form past eps 35); one wave
+  // per SIMD past eps 40 (accumulators in AGPRs)
+  std::vector<Variant> vs = {
+      {"nested_C8_D6", k_wide<E, 8, false, 6>, 64, 4},
+      {"nested_C8_D6_2wg", k_wide<E, 8, false, 6>, 64, 8},
+      {"nested_C8_D4", k_wide<E, 8, false, 4>, 64, 4},
+  };
+#endif
+
 
 
 
