@@ -175,3 +175,30 @@ def test_gloo_balance_round(world, name):
         assert p.exitcode == 0
     assert all(r[1] and r[2] for r in res), res
     assert len({r[3] for r in res}) == 1
+
+
+def test_fallback_moves_the_donor_tile_nearest_the_receiver():
+    """No donor tile borders a receiver (a neutral rank sits between them):
+    the policy's fallback moves the donor tile nearest (Manhattan; the BFS
+    distance map of nlh_plan.cpp) to the receiver's tiles, lowest index first
+    on ties; deterministic."""
+    # 6 x 1: receiver 0 | neutral 1 | donor 2 x 4
+    moved, new = N.balance_owner((6, 1), 3, np.array([0, 1, 2, 2, 2, 2], np.int32), [1.0, 17.0, 33.0])
+    assert moved == 2 and new.tolist() == [0, 1, 0, 0, 2, 2]
+    # 5 x 5: receiver in one corner, donor block in the far corner, neutral between
+    tx = ty = 5
+    own = np.ones(tx * ty, np.int32)
+    own[0] = 0
+    for gy in range(3, 5):
+        for gx in range(3, 5):
+            own[gx + gy * tx] = 2
+    busy = [1.0, 20.5, 40.0]  # rank 1 exactly at the mean: neither donor nor receiver
+    moved, new = N.balance_owner((tx, ty), 3, own, busy)
+    assert moved >= 1
+    got = [t for t in range(tx * ty) if own[t] == 2 and new[t] == 0]
+    # the donor tile nearest tile 0 (Manhattan), lowest index on ties: (3, 3)
+    dist = {t: (t % tx) + (t // tx) for t in range(tx * ty) if own[t] == 2}
+    first = min(dist, key=lambda t: (dist[t], t))
+    assert first in got
+    again = N.balance_owner((tx, ty), 3, own, busy)
+    assert again[0] == moved and np.array_equal(again[1], new)
