@@ -84,12 +84,17 @@ int main(int argc, char **argv) {
   // only (no LDS reads, no vmcnt waits, no stores, no DMA)
   std::vector<Variant> vs = {
       {"split_D8_B4", k_pair_split<E, 8, 0, 4>, 128, 4, 128 - 2 * E},
-      {"abl8_no_barrier", k_pair_split<E, 8, 8, 4>, 128, 4, 128 - 2 * E},
-      {"abl_valu_only", k_pair_split<E, 8, 452, 4>, 128, 4, 128 - 2 * E},
-      {"abl_valu_only_no_barrier", k_pair_split<E, 8, 460, 4>, 128, 4, 128 - 2 * E},
-      {"abl8_no_barrier_B8", k_pair_split<E, 8, 8, 8>, 128, 4, 128 - 2 * E},
-      {"split_D8_B8", k_pair_split<E, 8, 0, 8>, 128, 4, 128 - 2 * E},
+      {"lag2_D8_B4", k_pair_split<E, 8, 0, 4, false, 2>, 128, 4, 128 - 2 * E},
+      {"lag2_D4_B2", k_pair_split<E, 4, 0, 2, false, 2>, 128, 4, 128 - 2 * E},
+      {"lag3_D4_B2", k_pair_split<E, 4, 0, 2, false, 3>, 128, 4, 128 - 2 * E},
+      {"lag2_D6_B4", k_pair_split<E, 6, 0, 4, false, 2>, 128, 4, 128 - 2 * E},
+      {"split_D4_B2", k_pair_split<E, 4, 0, 2>, 128, 4, 128 - 2 * E},
+      {"split_D8_B4_again", k_pair_split<E, 8, 0, 4>, 128, 4, 128 - 2 * E},
+      {"lag2_D8_B4_again", k_pair_split<E, 8, 0, 4, false, 2>, 128, 4, 128 - 2 * E},
+      {"lag2_D4_B2_again", k_pair_split<E, 4, 0, 2, false, 2>, 128, 4, 128 - 2 * E},
   };
+
+
 
 
 
