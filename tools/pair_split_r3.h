@@ -1,107 +1,16 @@
-// nlh_pair.h -- two explicit-Euler steps per pass over HBM (temporal
-// blocking of the reference's do_work loop, src/2d_nonlocal_serial.cpp:273-303:
-// u^{t+1} = u^t + dt*L_h[u^t] applied twice, production mode, no source term).
-//
-// One 64-lane wave per (strip, segment), like k_fast (nlh_fast.h), but every
-// u^t row streamed HBM -> LDS feeds TWO nested-window sweeps:
-//
-//   stage 1: u^{t+1} over the 64*R columns x0-E .. x0-E+64R (the strip plus an
-//            E-wide halo on both sides), rows Y0-E .. Y1+E; values outside the
-//            lattice are forced to 0 (the reference's zero boundary) and each
-//            finished row is written to one of two LDS row buffers;
-//   stage 2: the same sweep over those u^{t+1} rows, one row behind stage 1,
-//            emitting u^{t+2} for the 64R-2E columns x0 .. x0+64R-2E and rows
-//            Y0 .. Y1.
-//
-// u^{t+1} never touches HBM: per two steps the kernel reads u^t (with a 2E
-// halo) and writes u^{t+2} once, about half the single-step traffic.
-//
-// Nested windows with a shared core.  A lane owns two adjacent columns a, b
-// and reads the 2E+2 values w[0..2E+1] around them.  With the core
-// K_L = w[E+1-L] + .. + w[E+L]:  H_L(a) = K_L + w[E-L],  H_L(b) = K_L + w[E+1+L],
-// evaluated only at the levels L the disk uses; 2E-1 + 2*levels adds per row
-// instead of 4E (25 instead of 32 at E = 8).  The accumulator of the output
-// E rows ahead receives its first term from this row (level 0, d = +E), so it
-// is assigned and never has to be zeroed.
-//
-// Centre fold: u' = u + alpha*(S - N u) = alpha*(S + (1/alpha - N) u), so the
-// centre value is added to its own accumulator (kc = 1/alpha - N) when its row
-// arrives and no centre rows have to be kept.  The extra rounding is a few ulp
-// of the field scale; alpha == 0 never reaches this kernel.
-//
-// Iteration i: DMA u^t row i+D -> wait for row i -> ds_read the u^{t+1}
-// window of row i-2E-1 (written by the previous iteration) and the u^t
-// window of row i -> stage-2 math (covers the LDS latency of the u^t window)
-// -> stage-1 math -> ds_write u^{t+1} row i-2E.  No LDS write->read round
-// trip sits on the critical path.
+// pair_split_r3.h -- frozen round-3 k_pair_split (one row per scatter), kept for
+// the tools/pair_bench.hip comparison with the row-pair kernel of nlh_pair.h.
 #pragma once
-
-#include "nlh_device.h"
-#include "nlh_kernel_common.h"
-
+#include "nlh_pair.h"
 namespace nlh {
-
-constexpr int kPairSplitD = 8;  // k_pair_split: rows in flight beyond the next block
-constexpr int kPairSplitB = 4;  // k_pair_split: rows per barrier
-
-// some row offset d of the disk has half-width len(d) == L
-__host__ __device__ constexpr bool pair_level_used(int E, int L) {
-  for (int d = 0; d <= E; ++d)
-    if (clen(E, d) == L) return true;
-  return false;
-}
-
-// Row pairs.  Rows are scattered in pairs, A (even row) then B (the next
-// row).  Where the disk's half-width is the same at two adjacent row offsets,
-// len(d) == len(d-1) > 0, the output row o = A + d receives H_L(A) (offset d)
-// and H_L(B) (offset d-1) of the same level L: row A skips that tap and row B
-// adds the pair sum H_L(A) + H_L(B) once -- one extra add per shared level
-// serves every such offset.  E = 8: offsets -4, -2, -1, 2, 3, 5 (levels 6 and
-// 7), 4 adds fewer per row pair and column (30 instead of 34).
-__host__ __device__ constexpr int pair_abs(int d) { return d < 0 ? -d : d; }
-__host__ __device__ constexpr bool pair_shared(int E, int d) {
-  return d > -E && d <= E && clen(E, pair_abs(d)) > 0 && clen(E, pair_abs(d)) == clen(E, pair_abs(d - 1));
-}
-__host__ __device__ constexpr bool pair_level_shared(int E, int L) {
-  for (int d = -E; d <= E; ++d)
-    if (pair_shared(E, d) && clen(E, pair_abs(d)) == L) return true;
-  return false;
-}
-__host__ __device__ constexpr bool pair_rows(int E) {
-  for (int d = -E; d <= E; ++d)
-    if (pair_shared(E, d)) return true;
-  return false;
-}
-// accumulator slots: the 2E+1 output rows a row touches, one more with row
-// pairs so that the unrolled period is even and no pair straddles it
-__host__ __device__ constexpr int pair_slots(int E) { return pair_rows(E) ? 2 * E + 2 : 2 * E + 1; }
-
-// window of 2E+R values starting at p (16-B aligned) into w
-template <int E, int R>
-__device__ __forceinline__ void pair_window(const double *p, double (&w)[R + 2 * E]) {
-  constexpr int NB = (R + 2 * E + 1) / 2;
-  const double2 *rp = reinterpret_cast<const double2 *>(p);
-  double buf[2 * NB];
-#pragma unroll
-  for (int k = 0; k < NB; ++k) {
-    const double2 v = rp[k];
-    buf[2 * k] = v.x;
-    buf[2 * k + 1] = v.y;
-  }
-#pragma unroll
-  for (int k = 0; k < R + 2 * E; ++k) w[k] = buf[k];
-}
-
 // Nested windows of the lane's two columns scattered into the accumulators
 // of the 2E+1 output rows this input row touches (slot of output row
 // input+d = (QA + d) mod P; QA = the input row's own slot), plus the folded
-// centre term.  ROLE 0: a lone row (no row pairs at this E); 1: row A of a
-// pair (shared taps left to B, its shared levels kept in hs); 2: row B (the
-// pair sums at the shared taps).
-template <int E, int QA, int ROLE>
-__device__ __forceinline__ void pair_scatter(const double (&w)[2 * E + 2], double (&acc)[2][pair_slots(E)],
-                                             double kc, double (&hs)[2][E + 1]) {
-  constexpr int P = pair_slots(E);
+// centre term.
+template <int E, int QA>
+__device__ __forceinline__ void pair_scatter_r3(const double (&w)[2 * E + 2], double (&acc)[2][2 * E + 1],
+                                             double kc) {
+  constexpr int P = 2 * E + 1;
   constexpr int SF = (QA + E) % P;      // d = +E: first term of that output row
   constexpr int SL = (QA + P - E) % P;  // d = -E: last term
   acc[0][SF] = w[E];
@@ -117,76 +26,24 @@ __device__ __forceinline__ void pair_scatter(const double (&w)[2 * E + 2], doubl
     if constexpr (pair_level_used(E, Lv)) {
       const double ha = core + w[E - Lv];
       const double hb = core + w[E + 1 + Lv];
-      constexpr bool shl = ROLE != 0 && pair_level_shared(E, Lv);
-      double pa = ha, pb = hb;
-      if constexpr (shl && ROLE == 1) {
-        hs[0][Lv] = ha;
-        hs[1][Lv] = hb;
-      } else if constexpr (shl && ROLE == 2) {
-        pa = hs[0][Lv] + ha;
-        pb = hs[1][Lv] + hb;
-      }
       auto tap = [&](auto dc) {
         constexpr int d = decltype(dc)::value - E;
-        constexpr int s = (QA + d + P) % P;
-        if constexpr (clen(E, pair_abs(d)) == Lv) {
-          if constexpr (ROLE == 1 && pair_shared(E, d)) {
-            // row B adds the pair sum
-          } else if constexpr (ROLE == 2 && pair_shared(E, d + 1)) {
-            acc[0][s] += pa;
-            acc[1][s] += pb;
-          } else {
-            acc[0][s] += ha;
-            acc[1][s] += hb;
-          }
+        if constexpr (clen(E, d < 0 ? -d : d) == Lv) {
+          acc[0][(QA + d + P) % P] += ha;
+          acc[1][(QA + d + P) % P] += hb;
         }
       };
-      static_for<2 * E + 1>(tap);
+      static_for<P>(tap);
     }
   };
   static_for<E>(level);
   acc[0][QA] = fma(kc, w[E], acc[0][QA]);
   acc[1][QA] = fma(kc, w[E + 1], acc[1][QA]);
 }
-
-// ABL: timing-decomposition masks for the tools/ harness (tools/pair_bench.hip).
-// libnlh instantiates ABL = 0 only (tests/test_capi.py checks the library's
-// kernel symbols); with ABL != 0 the results are meaningless.  k_pair_split:
-// 2 = no HBM traffic (no DMA, no stores; same instruction stream otherwise),
-// 4 = windows from registers (no LDS window reads), 8 = no s_barrier,
-// 16 = no u^{t+1} LDS writes, 32 = no per-row range checks (rows past the
-// segment end computed too), 64 = no vmcnt waits for the DMA'd rows, 128 = no
-// output stores, 256 = no DMA, 512 = non-temporal stores, 1024 = non-temporal DMA
-
-// k_pair_split: the two stages of k_pair on the two waves of one workgroup,
-// synchronised once per block of B rows (s_barrier):
-//   wave 0 (stage 1): u^t row i from the LDS ring -> u^{t+1} row i-2E into a
-//                     2B-row LDS ring;
-//   wave 1 (memory + stage 2): LDS-DMA of u^t row i+B+D (and, at each block
-//                     end, the wait for the next block's rows, so wave 0
-//                     never waits on HBM), stage 2 on u^{t+1} row i-2E-B (the
-//                     block wave 0 finished before the last barrier), and the
-//                     u^{t+2} store.
-// Each wave holds ONE accumulator set (2 x (2E+1) doubles): at the two waves
-// per SIMD of k_pair a workgroup owns a segment twice as tall, so less of the
-// 4E / 2E rows of redundant halo work per segment (4 workgroups per CU
-// measured best, see nlh_api.cpp); one barrier per B rows lets per-row
-// jitter of the two waves average out.  Same arithmetic and order as
-// k_pair: bitwise equal results.
-//
-// TEST (manufactured source, sum_local_test :235-252, in the fast form
-// b(x,t) = -(2 pi st_t) W0(x) - ct_t L_h[W0](x) with the precomputed plane
-// L_h[W0] of k_fast): wave 1 also DMAs, with u^t row i, the L_h[W0] row and
-// the sin(2 pi y dh) entry of u^{t+1} row i-2E.  Stage 1 adds dt*b(t) to
-// u^{t+1} and writes (dt/alpha)*b(t+1) beside it into a second 2B-row ring;
-// stage 2 folds that into the centre accumulator of the same row, so
-// u^{t+2} = alpha*(S + kc u^{t+1} + (dt/alpha) b(t+1)).  L_h[W0] is read once
-// per two steps.
 template <int E, int D, int ABL = 0, int B = kPairSplitB, bool TEST = false>
-__global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) {
+__global__ __launch_bounds__(128, 2) void k_pair_split_r3(RectList L, StepConst C) {
   constexpr int R = 2;
-  constexpr int P = pair_slots(E);      // accumulator slots = rows per unrolled period
-  constexpr bool PAIRS = (P & 1) == 0;  // rows scattered in pairs (even row = A)
+  constexpr int P = 2 * E + 1;
   constexpr int W1 = 64 * R;
   constexpr int WO = W1 - 2 * E;
   constexpr int NW = R + 2 * E;
@@ -207,7 +64,6 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
   static_assert((B & (B - 1)) == 0, "B must be a power of two");
   static_assert(D * GA + D + 1 < 64, "vmcnt range");
   static_assert(WO >= 64, "strip too narrow for this eps");
-  static_assert(P <= 2 * E + B, "the peeled iterations 0 .. P-1 carry no u^{t+1} row");
 
   __shared__ __attribute__((aligned(16))) double ring[K * RW + U1R * U1W + (TEST ? U1R * U1W + K * LWW + 2 * K : 0)];
   double *const u1buf = ring + K * RW;
@@ -270,7 +126,6 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
   for (int c = 0; c < R; ++c)
 #pragma unroll
     for (int j = 0; j < P; ++j) acc[c][j] = 0.0;
-  double hs[R][E + 1];  // row A's windows at the shared levels, until row B
 
   // barriers: one prologue barrier, then one after every iteration i with
   // i % B == B-1, for i = 0 .. i_last (wave 0 stops computing at n_in - 1)
@@ -291,13 +146,13 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
     for (int b = 0; b < n_in; b += P) {
       auto body = [&](auto qc) {
         constexpr int q = decltype(qc)::value;
-        constexpr int so = (q + P - E) % P;  // output row i - E completes
+        constexpr int so = (q + E + 1) % P;
         const int i = b + q;
         if constexpr ((ABL & 32) == 0)
           if (i >= n_in) return;
         double w[NW];
         window(ring + ((bs + q) & (K - 1)) * RW + R * lane, w);
-        pair_scatter<E, q, PAIRS ? 1 + (q & 1) : 0>(w, acc, kc, hs);
+        pair_scatter_r3<E, q>(w, acc, kc);
         if ((ABL & 32) != 0 || i >= 2 * E) {
           const int m = i - 2 * E;
           const int gy = gy1first + ydir * m;
@@ -406,8 +261,8 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
     for (int b = P; b <= i_last; b += P) {
       auto body = [&](auto qc) {
         constexpr int q = decltype(qc)::value;
-        constexpr int q2 = ((q - 2 * E - B) % P + P) % P;  // slot of row m2 = i - 2E - B (same parity as i)
-        constexpr int so = (q2 + P - E) % P;
+        constexpr int q2 = ((q + 1 - B) % P + P) % P;  // slot of row m2 = i - 2E - B
+        constexpr int so = (q2 + E + 1) % P;
         const int i = b + q;
         if constexpr ((ABL & 32) == 0)
           if (i > i_last) return;
@@ -418,7 +273,7 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
         const int m2 = i - 2 * E - B;
         double w2[NW];
         window(u1buf + (m2 & (U1R - 1)) * U1W + R * lane, w2);
-        pair_scatter<E, q2, PAIRS ? 1 + (q2 & 1) : 0>(w2, acc, kc, hs);
+        pair_scatter_r3<E, q2>(w2, acc, kc);
         if constexpr (TEST) {  // (dt/alpha) b(t+1) at the centre row of the output
           const double *qr = qbuf + (m2 & (U1R - 1)) * U1W + R * lane + E;
           acc[0][q2] += qr[0];
@@ -451,43 +306,4 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
     wait_vmcnt<0>();  // drain the clamped tail DMAs and the stores
   }
 }
-
-// pass variants libnlh launches (the host picks one per solver):
-//   1 production, 16-slot rings (D = 8, B = 4)   -- default
-//   6 production, 8-slot rings (D = 4, B = 2)    -- NLH_PAIR_SPLIT=4 (tuning)
-//   5 test mode, 8-slot rings (D = 4, B = 2)     -- default in test mode
-//   4 test mode, 16-slot rings (D = 8, B = 4)    -- NLH_PAIR_TEST=0 (tuning)
-// All four are the same arithmetic in the same order (bitwise equal fields).
-// Resident workgroups per CU (register/LDS-limited) for the host's choice of
-// segment height; 0 for an unknown variant
-template <int E>
-int pair_blocks_per_cu_e(int variant) {
-  int n = 0;
-  hipError_t e = hipErrorInvalidValue;
-  if (variant == 1) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_pair_split<E, kPairSplitD>, 128, 0);
-  else if (variant == 6) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_pair_split<E, 4, 0, 2>, 128, 0);
-  else if (variant == 5)
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_pair_split<E, 4, 0, 2, true>, 128, 0);
-  else if (variant == 4)
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_pair_split<E, kPairSplitD, 0, kPairSplitB, true>, 128, 0);
-  return e == hipSuccess ? n : 0;
-}
-
-template <int E>
-int launch_pair_e(const RectList &rl, const StepConst &c, int variant, hipStream_t st) {
-  if (variant == 1)
-    hipLaunchKernelGGL((k_pair_split<E, kPairSplitD>), dim3(rl.nwork), dim3(128), 0, st, rl, c);
-  else if (variant == 6)
-    hipLaunchKernelGGL((k_pair_split<E, 4, 0, 2>), dim3(rl.nwork), dim3(128), 0, st, rl, c);
-  else if (variant == 5)
-    hipLaunchKernelGGL((k_pair_split<E, 4, 0, 2, true>), dim3(rl.nwork), dim3(128), 0, st, rl, c);
-  else if (variant == 4)
-    hipLaunchKernelGGL((k_pair_split<E, kPairSplitD, 0, kPairSplitB, true>), dim3(rl.nwork), dim3(128), 0, st,
-                       rl, c);
-  else
-    return (int)hipErrorInvalidValue;
-  const hipError_t e = hipGetLastError();
-  return e == hipSuccess ? 0 : (int)e;
-}
-
 }  // namespace nlh

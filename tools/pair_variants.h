@@ -1,13 +1,13 @@
 // pair_variants.h -- alternate two-step pass designs kept for the timing
 // harness (tools/pair_bench.hip) only; libnlh ships k_pair_split
-// (nonlocalheatequation_amd/csrc/nlh_pair.h).  All three are bitwise equal to
+// (nonlocalheatequation_amd/csrc/nlh_pair.h).  All three are bitwise equal to the round-3
 // k_pair_split; DESIGN.md section 4 records why k_pair_split won.
 //   k_pair     one wave runs both stages (two accumulator sets per lane)
 //   k_pair_pf  k_pair_split with the next row's LDS window read ahead
 //   k_pair_mw  k_pair_split plus a third wave for all HBM traffic
 #pragma once
 
-#include "nlh_pair.h"
+#include "pair_split_r3.h"
 
 namespace nlh {
 
@@ -124,7 +124,7 @@ __global__ __launch_bounds__(64, (E <= 9 ? 2 : 1)) void k_pair(RectList L, StepC
       if constexpr (EARLY) pair_window<E, R>(ring + slot * RW + R * lane, w);
 
       // stage 2: u^{t+1} row m2 -> u^{t+2} row m2 - E complete
-      pair_scatter<E, q>(w2, acc2, kc);
+      pair_scatter_r3<E, q>(w2, acc2, kc);
       if (m2 >= 2 * E) {
         const double o0 = alpha * acc2[0][so];
         const double o1 = alpha * acc2[1][so];
@@ -140,7 +140,7 @@ __global__ __launch_bounds__(64, (E <= 9 ? 2 : 1)) void k_pair(RectList L, StepC
 
       // stage 1: u^t row i -> u^{t+1} row m = i - 2E complete
       if constexpr (!EARLY) pair_window<E, R>(ring + slot * RW + R * lane, w);
-      pair_scatter<E, q>(w, acc1, kc);
+      pair_scatter_r3<E, q>(w, acc1, kc);
       if (i >= 2 * E) {
         const int m = i - 2 * E;
         const int gy = gy1first + ydir * m;
@@ -249,7 +249,7 @@ __global__ __launch_bounds__(128, 2) void k_pair_pf(RectList L, StepConst C) {
         const bool bend = (i & (B - 1)) == B - 1;
         const bool more = i + 1 < n_in;
         if (more && !bend) pair_window<E, R>(ring_row(bs + q + 1), wb[ns]);
-        pair_scatter<E, q>(wb[cs], acc, kc);
+        pair_scatter_r3<E, q>(wb[cs], acc, kc);
         if (i >= 2 * E) {
           const int m = i - 2 * E;
           const int gy = gy1first + ydir * m;
@@ -317,7 +317,7 @@ __global__ __launch_bounds__(128, 2) void k_pair_pf(RectList L, StepConst C) {
         const bool bend = (i & (B - 1)) == B - 1;
         const bool more = i + 1 <= i_last;
         if (more && !bend) pair_window<E, R>(u1_row(m2 + 1), wb[ns]);
-        pair_scatter<E, q2>(wb[cs], acc, kc);
+        pair_scatter_r3<E, q2>(wb[cs], acc, kc);
         if (m2 >= 2 * E) {
           const double o0 = alpha * acc[0][so];
           const double o1 = alpha * acc[1][so];
@@ -423,7 +423,7 @@ __global__ __launch_bounds__(192, 3) void k_pair_mw(RectList L, StepConst C) {
         if (i >= n_in) return;
         double w[NW];
         pair_window<E, R>(ring + ((bs + q) & (K - 1)) * RW + R * lane, w);
-        pair_scatter<E, q>(w, acc, kc);
+        pair_scatter_r3<E, q>(w, acc, kc);
         if (i >= 2 * E) {
           const int m = i - 2 * E;
           const int gy = gy1first + ydir * m;
@@ -462,7 +462,7 @@ __global__ __launch_bounds__(192, 3) void k_pair_mw(RectList L, StepConst C) {
         const int m2 = i - 2 * E - B;
         double w2[NW];
         pair_window<E, R>(u1buf + (m2 & (U1R - 1)) * U1W + R * lane, w2);
-        pair_scatter<E, q2>(w2, acc, kc);
+        pair_scatter_r3<E, q2>(w2, acc, kc);
         if (m2 >= 2 * E) {
           const int k = m2 - 2 * E;
           *reinterpret_cast<double2 *>(obuf + (k & (U1R - 1)) * W1 + R * lane) =

@@ -80,9 +80,10 @@ int main(int argc, char **argv) {
   // rows ahead (k_wide PA), at DMA depths 6 and 8
 #if WB_E <= 32
   std::vector<Variant> vs = {
-      {"prod_C8_D6_PA2", k_wide<E, 8, false, 6, 0, 1, false, 16, true, true, 2, true>, 64, 8},
-      {"ils_C8_D6_PA2", k_wide<E, 8, false, 6, 0, 1, false, 16, true, true, 2, true, true>, 64, 8},
       {"ils_nts", k_wide<E, 8, false, 6, 0, 1, false, 16, true, true, 2, true, true, true>, 64, 8},
+      {"ils_nts_rp", k_wide<E, 8, false, 6, 0, 1, false, 16, true, true, 2, true, true, true, true>, 64, 8},
+      {"ils_nts_again", k_wide<E, 8, false, 6, 0, 1, false, 16, true, true, 2, true, true, true>, 64, 8},
+      {"ils_nts_rp_again", k_wide<E, 8, false, 6, 0, 1, false, 16, true, true, 2, true, true, true, true>, 64, 8},
   };
 #else
   // nested windows, 8-row chunks (the production form past eps 35); one wave
@@ -93,12 +94,6 @@ int main(int argc, char **argv) {
       {"nested_C8_D4", k_wide<E, 8, false, 4>, 64, 4},
   };
 #endif
-
-
-
-
-
-
 
   std::vector<double> ref((size_t)n * n), got((size_t)n * n);
   hipEvent_t e0, e1;
