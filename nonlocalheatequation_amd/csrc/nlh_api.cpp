@@ -153,7 +153,7 @@ constexpr EnvKnob kEnvKnobs[] = {
     {"NLH_INT_PER_CU", 0, 64},     // interior workgroups per CU beside an exchange
     {"NLH_SCHED", 0, 2},           // where the edge bands run
     {"NLH_COMM_PRIO", 0, 1},       // exchange streams at the highest priority
-    {"NLH_PAIR_SPLIT", 1, 4},      // 4: production pass with 8-slot rings
+    {"NLH_PAIR_SPLIT", 1, 4},      // 1: production pass with 16-slot rings (4: 8-slot, the default)
     {"NLH_PAIR_CU", 1, 16},        // pass workgroups per CU the segments are sized for
     {"NLH_PAIR_TEST", 0, 1},       // 0: test-mode pass with 16-slot rings
     {"NLH_PITCH_PAD", 0, 1024},    // extra doubles per padded row
@@ -253,7 +253,9 @@ struct nlh_solver {
   bool weighted = false;  // k_weighted: non-constant influence function
   double *d_wt = nullptr, *d_qj = nullptr;  // J tables (influence != 0)
   int halo = 0;       // halo rows/columns held per block: eps, or 2*eps with pair
-  int pair_split = 1;  // production k_pair_split rings: 1 = D8/B4 (default), 6 = D4/B2 (NLH_PAIR_SPLIT=4)
+  // production k_pair_split rings: 6 = D4/B2 (default; with row pairs 444-450 vs 438-446 G
+  // node/s for D8/B4 at C2, profiles/r03/rowpairs/pair_rows_sweep.jsonl), 1 = D8/B4 (NLH_PAIR_SPLIT=1)
+  int pair_split = 6;
   // test-mode pass: 5 = k_pair_split<TEST> with 8-slot rings (D=4, B=2; 322 vs
   // 287 G node/s at C2 for the production rings, profiles/r02/tune_test.jsonl),
   // 4 = D=8, B=4 (NLH_PAIR_TEST=0)
@@ -937,7 +939,7 @@ int create_impl(const nlh_params *pin, nlh_solver *s, ncclComm_t reuse_comm = nu
   if (const char *cp = std::getenv("NLH_COMM_PRIO"))
     if (std::atoi(cp) != 0) HIP_TRY(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
   if (const char *ps = std::getenv("NLH_PAIR_SPLIT"))
-    if (std::atoi(ps) == 4) s->pair_split = 6;  // k_pair_split with 8-slot rings (variant 6)
+    if (std::atoi(ps) == 1) s->pair_split = 1;  // k_pair_split with 16-slot rings (variant 1)
   if (const char *pc = std::getenv("NLH_PAIR_CU")) s->pair_cu = std::max(1, std::atoi(pc));
   if (const char *pt = std::getenv("NLH_PAIR_TEST")) s->pair_test = std::atoi(pt) == 0 ? 4 : 5;
   s->halo = rv.halo;

@@ -453,8 +453,8 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
 }
 
 // pass variants libnlh launches (the host picks one per solver):
-//   1 production, 16-slot rings (D = 8, B = 4)   -- default
-//   6 production, 8-slot rings (D = 4, B = 2)    -- NLH_PAIR_SPLIT=4 (tuning)
+//   6 production, 8-slot rings (D = 4, B = 2)    -- default
+//   1 production, 16-slot rings (D = 8, B = 4)   -- NLH_PAIR_SPLIT=1 (tuning)
 //   5 test mode, 8-slot rings (D = 4, B = 2)     -- default in test mode
 //   4 test mode, 16-slot rings (D = 8, B = 4)    -- NLH_PAIR_TEST=0 (tuning)
 // All four are the same arithmetic in the same order (bitwise equal fields).

@@ -54,6 +54,21 @@ __host__ __device__ constexpr int wide_tap_dy(int E, int L, int t) {
   return 0;
 }
 
+// Row pairs (RP): rows c (even, A) and c+1 (B) of a chunk reach output a at
+// row offsets dy and dy+1.  Where len(|dy|) == len(|dy+1|) > 0 both add the
+// same level: row A skips that tap and row B adds H_L(A) + H_L(B) once, one
+// extra add per shared level (E = 32: 26 of the 128 taps of a row pair become
+// 6 pair sums -- 20 adds fewer per row pair and column).
+__host__ __device__ constexpr bool wide_shared(int E, int dy) {
+  return dy >= -E && dy < E && clen(E, dy < 0 ? -dy : dy) > 0 &&
+         clen(E, dy < 0 ? -dy : dy) == clen(E, dy + 1 < 0 ? -dy - 1 : dy + 1);
+}
+__host__ __device__ constexpr bool wide_level_shared(int E, int L) {
+  for (int dy = -E; dy < E; ++dy)
+    if (wide_shared(E, dy) && clen(E, dy < 0 ? -dy : dy) == L) return true;
+  return false;
+}
+
 // the last level < L whose row window feeds some output (0: the centre column)
 __host__ __device__ constexpr int wide_prev_used(int E, int L) {
   for (int l = L - 1; l > 0; --l)
@@ -122,7 +137,8 @@ __device__ __forceinline__ double wave_prefix_sum(double x) {
 // basic block and the scan's dependent DPP/add chain interleaves with the
 // taps instead of running alone.  Same arithmetic: bitwise equal.
 template <int E, int CH, bool TEST, int D = kWideD, int ABL = 0, int PIN = 1, bool AB = false, int OBP = 16,
-          bool SPLIT8 = true, bool PS = false, int PA = 0, bool PSPLIT = false, bool ILS = false, bool NTS = false>
+          bool SPLIT8 = true, bool PS = false, int PA = 0, bool PSPLIT = false, bool ILS = false, bool NTS = false,
+          bool RP = false>
 __global__ __launch_bounds__(64, 1) void k_wide(RectList L, StepConst C) {
   constexpr int W = 64;                 // output columns per strip
   constexpr int EP = (E + 1) & ~1;      // staged halo columns per side (16-B rows)
@@ -141,6 +157,7 @@ __global__ __launch_bounds__(64, 1) void k_wide(RectList L, StepConst C) {
   constexpr int NG = (E + kWideLG - 1) / kWideLG;  // level groups
   static_assert(D * G + CH < 64, "vmcnt range");
   static_assert(CH % PIN == 0, "rows per pin");
+  static_assert(!RP || (CH % 2 == 0 && PS && PA > 0), "row pairs: even chunks, prefix-ahead rows");
 
   static_assert(!PS || (RW <= 256 && !AB), "prefix-sum rows: at most four staged doubles per lane");
   static_assert(PA == 0 || (PS && PA < D), "prefix-ahead rows need prefix sums and landed rows");
@@ -256,6 +273,7 @@ __global__ __launch_bounds__(64, 1) void k_wide(RectList L, StepConst C) {
   double acc[NA];
 #pragma unroll
   for (int a = 0; a < NA; ++a) acc[a] = 0.0;
+  double hsv[E + 1];  // RP: row A's windows at the shared levels, until row B
 
   const double qs = TEST ? C.dt / alpha : 0.0;
   const int nchunk = (n_in + CH - 1) / CH;
@@ -364,9 +382,21 @@ __global__ __launch_bounds__(64, 1) void k_wide(RectList L, StepConst C) {
           constexpr int Lv = decltype(lc)::value + 1;
           if constexpr (wide_taps(E, Lv) > 0) {
             const double h = hp[Lv] - hm[Lv];
+            constexpr bool sh = RP && wide_level_shared(E, Lv);
+            double ps = h;
+            if constexpr (sh && c % 2 == 0)
+              hsv[Lv] = h;
+            else if constexpr (sh)
+              ps = hsv[Lv] + h;
             static_for<wide_taps(E, Lv)>([&](auto kk) __attribute__((always_inline)) {
               constexpr int dy = wide_tap_dy(E, Lv, decltype(kk)::value);
-              acc[c + E - dy] += h;
+              if constexpr (RP && c % 2 == 0 && wide_shared(E, dy)) {
+                // row B adds the pair sum
+              } else if constexpr (RP && c % 2 == 1 && wide_shared(E, dy - 1)) {
+                acc[c + E - dy] += ps;
+              } else {
+                acc[c + E - dy] += h;
+              }
             });
           }
         });
@@ -537,10 +567,17 @@ constexpr int wide_chunk_pa() { return E <= 32 ? 8 : wide_chunk<E>(); }
 template <int E>
 constexpr bool wide_ils() { return wide_pa<E>() > 0; }
 
+// ... and row pairs (RP) in production: C4 159.0 -> 165.4-167.0 G node/s in
+// tools/wide_bench.hip (profiles/r03/rowpairs/wide_rp.jsonl; 248 -> 254 VGPRs,
+// two waves per SIMD).  Test mode keeps RP off: at E = 32 its source terms
+// push RP past 256 VGPRs (one wave per SIMD)
+template <int E, bool TEST>
+constexpr bool wide_rp() { return !TEST && wide_pa<E>() > 0; }
+
 template <int E, bool TEST>
 int launch_wide_e(const RectList &rl, const StepConst &c, hipStream_t st) {
   hipLaunchKernelGGL((k_wide<E, wide_chunk_pa<E>(), TEST, kWideD, 0, 1, false, 16, true, wide_ps<E>(), wide_pa<E>(),
-                             (wide_pa<E>() > 0), wide_ils<E>(), wide_ils<E>()>),
+                             (wide_pa<E>() > 0), wide_ils<E>(), wide_ils<E>(), wide_rp<E, TEST>()>),
                      dim3(rl.nwork), dim3(64), 0, st, rl, c);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : (int)e;
@@ -553,7 +590,7 @@ int wide_blocks_per_cu_e() {
   int n = 0;
   const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
       &n, k_wide<E, wide_chunk_pa<E>(), false, kWideD, 0, 1, false, 16, true, wide_ps<E>(), wide_pa<E>(),
-             (wide_pa<E>() > 0), wide_ils<E>(), wide_ils<E>()>,
+             (wide_pa<E>() > 0), wide_ils<E>(), wide_ils<E>(), wide_rp<E, false>()>,
       64, 0);
   return e == hipSuccess ? n : 0;
 }

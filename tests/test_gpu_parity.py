@@ -388,8 +388,8 @@ def test_pair_segment_heights(oracle, seg):
 
 @pytest.mark.parametrize("eps", [3, 8, 12, 16])
 def test_pair_ring_variants_bitwise_equal(monkeypatch, eps):
-    """The production pass with 16-slot (default) and 8-slot rings
-    (NLH_PAIR_SPLIT=4) runs the same arithmetic in the same order: bitwise
+    """The production pass with 8-slot (default) and 16-slot rings
+    (NLH_PAIR_SPLIT=1) runs the same arithmetic in the same order: bitwise
     equal at equal segmentation."""
     rng = np.random.default_rng(3 + eps)
     nx, ny = 257, 190
