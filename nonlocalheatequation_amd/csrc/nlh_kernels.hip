@@ -583,10 +583,11 @@ NLH_PAIR_EXTERN(5) NLH_PAIR_EXTERN(6) NLH_PAIR_EXTERN(7) NLH_PAIR_EXTERN(8)
 NLH_PAIR_EXTERN(9) NLH_PAIR_EXTERN(10) NLH_PAIR_EXTERN(11) NLH_PAIR_EXTERN(12)
 NLH_PAIR_EXTERN(13) NLH_PAIR_EXTERN(14) NLH_PAIR_EXTERN(15) NLH_PAIR_EXTERN(16)
 
-// E = 13 and 15 spill registers in k_pair_split under hipcc 7.2 (and k_pair
-// runs one wave per SIMD there): the single-step k_fast is faster for them
-// (profiles/r01/pair_v4/tune_eps_split.jsonl)
-bool pair_supported(int E) { return (E >= 1 && E <= 12) || E == 14 || E == 16; }
+// E = 15 spills registers in k_pair_split under hipcc 7.2 (424 bytes of
+// scratch per lane): the single-step k_fast is faster there
+// (profiles/r01/pair_v4/tune_eps_split.jsonl).  E = 13 spilled too before
+// row pairs; with them it fits (230 VGPRs, two waves per SIMD)
+bool pair_supported(int E) { return (E >= 1 && E <= 14) || E == 16; }
 
 int pair_strip_width(int E) { return 128 - 2 * E; }
 

@@ -157,7 +157,7 @@ __global__ __launch_bounds__(64, 1) void k_wide(RectList L, StepConst C) {
   constexpr int NG = (E + kWideLG - 1) / kWideLG;  // level groups
   static_assert(D * G + CH < 64, "vmcnt range");
   static_assert(CH % PIN == 0, "rows per pin");
-  static_assert(!RP || (CH % 2 == 0 && PS && PA > 0), "row pairs: even chunks, prefix-ahead rows");
+  static_assert(!RP || (CH % 2 == 0 && (PA > 0 || !PS)), "row pairs: even chunks; prefix-ahead rows or nested windows");
 
   static_assert(!PS || (RW <= 256 && !AB), "prefix-sum rows: at most four staged doubles per lane");
   static_assert(PA == 0 || (PS && PA < D), "prefix-ahead rows need prefix sums and landed rows");
@@ -475,9 +475,21 @@ __global__ __launch_bounds__(64, 1) void k_wide(RectList L, StepConst C) {
               core = core + (pend + seg);
             else
               core = core + seg;
+            constexpr bool sh = RP && wide_level_shared(E, Lv);
+            double ps = core;
+            if constexpr (sh && c % 2 == 0)
+              hsv[Lv] = core;
+            else if constexpr (sh)
+              ps = hsv[Lv] + core;
             auto tap = [&](auto kk) __attribute__((always_inline)) {
               constexpr int dy = wide_tap_dy(E, Lv, decltype(kk)::value);
-              acc[c + E - dy] += core;
+              if constexpr (RP && c % 2 == 0 && wide_shared(E, dy)) {
+                // row B adds the pair sum
+              } else if constexpr (RP && c % 2 == 1 && wide_shared(E, dy - 1)) {
+                acc[c + E - dy] += ps;
+              } else {
+                acc[c + E - dy] += core;
+              }
             };
             static_for<wide_taps(E, Lv)>(tap);
           }
@@ -569,10 +581,13 @@ constexpr bool wide_ils() { return wide_pa<E>() > 0; }
 
 // ... and row pairs (RP) in production: C4 159.0 -> 165.4-167.0 G node/s in
 // tools/wide_bench.hip (profiles/r03/rowpairs/wide_rp.jsonl; 248 -> 254 VGPRs,
-// two waves per SIMD).  Test mode keeps RP off: at E = 32 its source terms
-// push RP past 256 VGPRs (one wave per SIMD)
+// two waves per SIMD), and on the nested windows past E = 40 (one wave per
+// SIMD there either way): eps 48 67.1 -> 67.5-67.9, eps 64 36.3 -> 39.7 G
+// (profiles/r03/rowpairs/wide{48,64}.jsonl).  E = 33..40 keep one-row taps
+// (two waves per SIMD at up to 256 VGPRs without them).  Test mode keeps RP
+// off: at E = 32 its source terms push RP past 256 VGPRs (one wave per SIMD)
 template <int E, bool TEST>
-constexpr bool wide_rp() { return !TEST && wide_pa<E>() > 0; }
+constexpr bool wide_rp() { return !TEST && (wide_pa<E>() > 0 || E > 40); }
 
 template <int E, bool TEST>
 int launch_wide_e(const RectList &rl, const StepConst &c, hipStream_t st) {

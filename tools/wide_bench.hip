@@ -79,19 +79,28 @@ int main(int argc, char **argv) {
   // variants: prefix-sum rows (production, PA = 0) and prefix rows built PA
   // rows ahead (k_wide PA), at DMA depths 6 and 8
 #if WB_E <= 32
+  // production (ILS + nt stores + row pairs) and row-pair variants of DMA
+  // depth D, prefix-ahead distance PA and chunk rows CH
   std::vector<Variant> vs = {
-      {"ils_nts", k_wide<E, 8, false, 6, 0, 1, false, 16, true, true, 2, true, true, true>, 64, 8},
-      {"ils_nts_rp", k_wide<E, 8, false, 6, 0, 1, false, 16, true, true, 2, true, true, true, true>, 64, 8},
-      {"ils_nts_again", k_wide<E, 8, false, 6, 0, 1, false, 16, true, true, 2, true, true, true>, 64, 8},
-      {"ils_nts_rp_again", k_wide<E, 8, false, 6, 0, 1, false, 16, true, true, 2, true, true, true, true>, 64, 8},
+      {"rp_C8_D6_PA2", k_wide<E, 8, false, 6, 0, 1, false, 16, true, true, 2, true, true, true, true>, 64, 8},
+      {"rp_C8_D8_PA2", k_wide<E, 8, false, 8, 0, 1, false, 16, true, true, 2, true, true, true, true>, 64, 8},
+      {"rp_C8_D6_PA3", k_wide<E, 8, false, 6, 0, 1, false, 16, true, true, 3, true, true, true, true>, 64, 8},
+      {"rp_C6_D6_PA2", k_wide<E, 6, false, 6, 0, 1, false, 16, true, true, 2, true, true, true, true>, 64, 8},
+      {"rp_C4_D6_PA2", k_wide<E, 4, false, 6, 0, 1, false, 16, true, true, 2, true, true, true, true>, 64, 8},
+      {"one_row_C8_D6_PA2", k_wide<E, 8, false, 6, 0, 1, false, 16, true, true, 2, true, true, true, false>, 64, 8},
+      {"rp_C8_D6_PA2_b", k_wide<E, 8, false, 6, 0, 1, false, 16, true, true, 2, true, true, true, true>, 64, 8},
+      {"rp_C8_D8_PA2_b", k_wide<E, 8, false, 8, 0, 1, false, 16, true, true, 2, true, true, true, true>, 64, 8},
+      {"rp_C8_D6_PA3_b", k_wide<E, 8, false, 6, 0, 1, false, 16, true, true, 3, true, true, true, true>, 64, 8},
+      {"rp_C6_D6_PA2_b", k_wide<E, 6, false, 6, 0, 1, false, 16, true, true, 2, true, true, true, true>, 64, 8},
   };
 #else
-  // nested windows, 8-row chunks (the production form past eps 35); one wave
-  // per SIMD past eps 40 (accumulators in AGPRs)
+  // nested windows, 8-row chunks (the production form past eps 35), one row
+  // at a time vs row pairs; one wave per SIMD past eps 40 (AGPRs)
   std::vector<Variant> vs = {
       {"nested_C8_D6", k_wide<E, 8, false, 6>, 64, 4},
-      {"nested_C8_D6_2wg", k_wide<E, 8, false, 6>, 64, 8},
-      {"nested_C8_D4", k_wide<E, 8, false, 4>, 64, 4},
+      {"nested_C8_D6_rp", k_wide<E, 8, false, 6, 0, 1, false, 16, true, false, 0, false, false, false, true>, 64, 4},
+      {"nested_C8_D6_b", k_wide<E, 8, false, 6>, 64, 4},
+      {"nested_C8_D6_rp_b", k_wide<E, 8, false, 6, 0, 1, false, 16, true, false, 0, false, false, false, true>, 64, 4},
   };
 #endif
 
