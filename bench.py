@@ -82,10 +82,12 @@ def host_cpu_share() -> int:
 
 
 def cpu_baseline(nthreads: int, nb: int = NB, eps: int = EPS, test: bool = False,
-                 budget_s: float = 15.0) -> dict:
+                 budget_s: float = 15.0, serial_budget_s: float = 8.0) -> dict:
     """Oracle restatement of 2d_nonlocal_async (np x np tiles, one task per
     tile per step, a barrier per step) on the same nb^2 / eps workload,
-    bounded to ~budget_s of wall time."""
+    bounded to ~budget_s of wall time, plus the single-core serial restatement
+    of 2d_nonlocal_serial on a lattice sized to
+    ~serial_budget_s."""
     import nonlocalheatequation_amd as N
     from oracle import oracle as O  # test infrastructure: baseline leg only
 
@@ -95,14 +97,31 @@ def cpu_baseline(nthreads: int, nb: int = NB, eps: int = EPS, test: bool = False
     u = O.test_init(p)
     tiles = max(1, nb // 128)  # 128 x 128-node tiles
     t1 = O.run_tiled(p, 1, tiles, tiles, u, nthreads)
-    steps = int(max(1, min(200, budget_s / max(t1, 1e-3) - 1)))
-    t = O.run_tiled(p, steps, tiles, tiles, u, nthreads)
+    if t1 > budget_s / 3:  # one step already fills the budget (C4's 8192^2 at eps 32): it is the sample
+        steps, t = 1, t1
+    else:
+        steps = int(max(1, min(200, budget_s / max(t1, 1e-3) - 1)))
+        t = O.run_tiled(p, steps, tiles, tiles, u, nthreads)
     rate = nb * nb * steps / t / 1e9
+    # single core: a square lattice of the same eps / mode sized from the
+    # tiled per-thread rate, one step of the serial restatement
+    per_thread = nb * nb * steps / t / max(1, nthreads)
+    side = int(min(nb, max(64, math.sqrt(serial_budget_s * per_thread)))) // 64 * 64
+    ps = O.params(side, side, eps, 1.0, eps ** 4 / (8.0 * side * side * N.disk_count(eps)), 1.0 / side, int(test))
+    us = O.test_init(ps)
+    t0 = time.perf_counter()
+    O.run(ps, 1, us, nthreads=1)
+    ts = time.perf_counter() - t0
+    serial = {"value": side * side / ts / 1e9, "unit": "Gnode-updates/s", "cores": 1,
+              "sample": f"{side}x{side} lattice, eps={eps}, test={int(test)}, 1 step ({ts:.1f} s), "
+                        f"oracle/nlh_oracle.c nlh_oracle_run on one thread (2d_nonlocal_serial restatement)"}
     return {"value": rate, "unit": "Gnode-updates/s", "cores": nthreads, "kind": "port",
             "host_cpus_visible": os.cpu_count(),
-            "sample": f"{nb}x{nb} lattice, eps={eps}, test={int(test)}, {steps} step(s) after 1 warm-up step "
-                      f"({t:.1f} s), {tiles}x{tiles} tiles on {nthreads} threads (the job's host CPU share), "
-                      f"oracle/nlh_oracle.c run_tiled (-O3 -ffp-contract=off)"}
+            "sample": f"{nb}x{nb} lattice, eps={eps}, test={int(test)}, {steps} step(s) "
+                      f"({t:.1f} s{'' if steps == 1 and t == t1 else ', after 1 warm-up step'}), "
+                      f"{tiles}x{tiles} tiles on {nthreads} threads (the job's host CPU share), "
+                      f"oracle/nlh_oracle.c run_tiled (-O3 -ffp-contract=off)",
+            "serial_1core": serial}
 
 
 def workload_key(nb, eps, strong, test) -> str:
@@ -247,6 +266,67 @@ def spawn_ranks(n: int) -> int:
     return rc
 
 
+def strong_reference(args) -> dict:
+    """T1 of the strong-scaling efficiency T1 / (N T_N): this bench on ONE GPU
+    over the same total lattice, run as a child process before this rank
+    touches the GPU (the other ranks wait in the rendezvous meanwhile)."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
+                        "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID")}
+    cmd = [sys.executable, os.path.abspath(__file__), "--gpus", "1", "--strong", "--lattice", str(args.lattice),
+           "--eps", str(args.eps), "--steps", str(args.steps), "--warmup", str(args.warmup),
+           "--kernel", args.kernel, "--influence", args.influence, "--pmc", "off", "--no-cpu-baseline"]
+    if args.test_mode:
+        cmd.append("--test-mode")
+    try:
+        r = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=900)
+    except (OSError, subprocess.SubprocessError) as e:
+        return {"error": f"1-GPU reference run failed: {e}"}
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    if r.returncode != 0 or not lines:
+        return {"error": f"1-GPU reference run exited {r.returncode}: {r.stderr[-400:]}"}
+    one = json.loads(lines[-1])
+    return {"ms_per_step": one["ms_per_step"], "value": one["value"], "build_id": one.get("build_id"),
+            "kernel_avg_us": one["roofline"]["kernel_avg_us"]}
+
+
+def scaling_fields(nranks: int, strong: bool, ms_per_step: float, t1=None, phases=None,
+                   comm_seen=None) -> dict:
+    """The N > 1 fields of the bench line (tests/test_bench.py checks the
+    schema on CPU):
+      nranks_seen        ranks of the RCCL communicator as RCCL reports them
+                         (ncclCommCount, identical on every rank; 1 without one)
+      exchange           per-pass phase times (nlh_phase_time, max over ranks):
+                         interior / band / exchange kernels, wall, and the
+                         exposed exchange = wall - interior
+      strong_efficiency  T1 / (N T_N), T1 from the 1-GPU run of the same lattice
+    """
+    out = {"nranks_seen": comm_seen if comm_seen else 1}
+    if phases:
+        P = max(1, phases["passes"])
+        per = {k: phases[k] / P for k in ("wall_ms", "interior_ms", "band_ms", "exchange_ms", "exposed_exchange_ms")}
+        out["exchange"] = {
+            "passes_timed": phases["passes"], "steps_per_pass": phases["steps"] / P,
+            "wall_ms_per_pass": per["wall_ms"], "interior_ms_per_pass": per["interior_ms"],
+            "band_ms_per_pass": per["band_ms"], "exchange_ms_per_pass": per["exchange_ms"],
+            "exposed_exchange_ms_per_pass": per["exposed_exchange_ms"],
+            "exposed_share_of_pass": per["exposed_exchange_ms"] / per["wall_ms"] if per["wall_ms"] > 0 else None,
+            "halo_bytes_sent_per_pass": phases.get("halo_bytes_sent"),
+            "over_ranks": "max",
+            "source": "nlh_phase_time: HIP event pairs on the streams the interior, edge-band and exchange "
+                      "(pack, grouped ncclSend/ncclRecv, unpack) run on, a separate untimed run after the "
+                      "timed region",
+        }
+    if strong and nranks > 1:
+        if t1 and "ms_per_step" in t1:
+            out["strong_efficiency"] = t1["ms_per_step"] / (nranks * ms_per_step)
+            out["strong_reference"] = dict(t1, n_gpus=1)
+        else:
+            out["strong_efficiency"] = None
+            out["strong_reference"] = t1
+    return out
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -259,12 +339,17 @@ def main() -> int:
                     help="continue the untimed warm-up until this much stepping has passed")
     ap.add_argument("--pmc", default="auto", choices=["auto", "off"],
                     help="auto: collect the roofline's PMC counters live (N=1, rocprofv3 on PATH)")
+    ap.add_argument("--phase-passes", type=int, default=50,
+                    help="passes of the untimed phase-timing run (exchange report; runs with several owners)")
     # secondary workloads (the default line is C2): --eps 32 --lattice 8192 is
     # C4; --lattice 32768 --strong is C3 (total lattice fixed as N grows);
     # --test-mode times the manufactured-solution step and reports its L2
     ap.add_argument("--eps", type=int, default=EPS)
     ap.add_argument("--lattice", type=int, default=NB, help="lattice edge per GPU (weak) or total (--strong)")
     ap.add_argument("--strong", action="store_true")
+    ap.add_argument("--blocks", default="",
+                    help="PXxPY block grid instead of the per-N default (one GPU under NLH_VIRTUAL_RANKS: "
+                         "e.g. --strong --lattice 32768 --blocks 2x4 runs C3's 8 ranks on one device)")
     ap.add_argument("--test-mode", action="store_true")
     # J(r) = 1 - r (problem_description.tex:159; not the BASELINE metric, whose J = 1)
     ap.add_argument("--influence", default="constant", choices=["constant", "linear"])
@@ -273,6 +358,17 @@ def main() -> int:
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         return spawn_ranks(args.gpus)
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world:
+        print(f"--gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+        return 2
+    nranks = world
+
+    # strong scaling: the 1-GPU time of the same lattice, before any GPU call here
+    t1 = strong_reference(args) if args.strong and nranks > 1 and rank == 0 else None
 
     wkey = workload_key(nb, eps, args.strong, args.test_mode) + ("_linear" if args.influence == "linear" else "")
     pmc_live = None
@@ -286,14 +382,6 @@ def main() -> int:
               file=sys.stderr)
         return 4
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.gpus != world:
-        print(f"--gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-        return 2
-    nranks = world
-
     dist = None
     if nranks > 1:
         import torch.distributed as dist  # control plane only (id broadcast, barrier, max)
@@ -303,6 +391,11 @@ def main() -> int:
             return 3
 
     px, py = decomposition(nranks)
+    if args.blocks:
+        px, py = (int(v) for v in args.blocks.lower().split("x"))
+        if nranks > 1 and px * py != nranks:
+            print(f"--blocks {args.blocks} needs one block per rank", file=sys.stderr)
+            return 2
     if args.strong:
         if nb % px or nb % py:
             print(f"--lattice {nb} is not divisible by the {px}x{py} block grid", file=sys.stderr)
@@ -325,16 +418,25 @@ def main() -> int:
                  rank=rank, nranks=nranks, tiles=(px, py), comm_id=comm_id, seg_rows=args.seg_rows,
                  influence=args.influence)
     info = s.info()
-    # every rank owns exactly one block of the px x py grid: the communicator
-    # and the plan both see all N ranks
-    owned = [info.owned_nodes]
+    # every rank owns exactly one block of the px x py grid, and the RCCL
+    # communicator itself (ncclCommCount / ncclCommUserRank, nlh_info) must
+    # see all N ranks, each once -- else the line would claim GPUs that did not
+    # take part
+    comm_seen = None
     if dist is not None:
         lst = [None] * nranks
-        dist.all_gather_object(lst, (info.owned_nodes, info.nblocks))
-        owned = [o for o, _ in lst]
+        dist.all_gather_object(lst, (info.owned_nodes, info.nblocks, info.comm_nranks, info.comm_rank))
+        owned = [o[0] for o in lst]
         if sum(owned) != nx * ny or any(o == 0 for o in owned):
             print(f"ranks own {owned} nodes of {nx * ny}", file=sys.stderr)
             return 3
+        counts = {o[2] for o in lst}
+        ranks_seen = sorted(o[3] for o in lst)
+        if counts != {nranks} or ranks_seen != list(range(nranks)):
+            print(f"RCCL communicator sizes {sorted(counts)} / ranks {ranks_seen}, expected {nranks} ranks",
+                  file=sys.stderr)
+            return 5
+        comm_seen = nranks
     s.test_init()
     # warm-up: W steps, then more until --warmup-ms of stepping has passed (the
     # clocks a sustained run holds); every rank runs the same count (rank 0's)
@@ -368,11 +470,11 @@ def main() -> int:
     t0 = time.perf_counter()
     s.run(args.steps)
     s.synchronize()
-    t1 = time.perf_counter()
+    t1_wall = time.perf_counter()
     k_ms, k_n = s.kernel_time()
     s.kernel_timing(False)
     barrier()
-    elapsed = t1 - t0
+    elapsed = t1_wall - t0
     if dist is not None:
         import torch
         t = torch.tensor([elapsed], dtype=torch.float64)
@@ -380,6 +482,27 @@ def main() -> int:
         elapsed = float(t.item())
 
     l2 = s.compute_l2(s.step_index) if args.test_mode else None  # after the timed region
+
+    # exchange report (several owners): a separate, untimed run with an event
+    # pair around every pass's interior, bands and exchange
+    phases = None
+    if (nranks > 1 or info.owners > 1) and args.phase_passes > 0:
+        barrier()
+        s.kernel_timing(3)
+        s.run(args.phase_passes * info.steps_per_pass)
+        s.synchronize()
+        ph = s.phase_time()
+        s.kernel_timing(False)
+        vals = [ph.wall_ms, ph.interior_ms, ph.band_ms, ph.exchange_ms, ph.exposed_exchange_ms]
+        if dist is not None:
+            import torch
+            tv = torch.tensor(vals, dtype=torch.float64)
+            dist.all_reduce(tv, op=dist.ReduceOp.MAX)
+            vals = tv.tolist()
+        phases = dict(zip(("wall_ms", "interior_ms", "band_ms", "exchange_ms", "exposed_exchange_ms"), vals),
+                      passes=ph.passes, steps=ph.steps, halo_bytes_sent=info.halo_bytes_sent)
+        barrier()
+
     total_nodes = nx * ny
     value = total_nodes * args.steps / elapsed / 1e9
     ms_per_step = elapsed * 1e3 / args.steps
@@ -437,14 +560,14 @@ def main() -> int:
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and nranks == 1 and args.influence == "constant":
-            # bounded sample: at most a 4096^2 lattice of the same eps / mode
-            cpu = cpu_baseline(host_cpu_share(), min(nb, NB), eps, args.test_mode)
+            # bounded sample on the workload's own lattice (one step when that
+            # fills the budget: C4) and a single-core serial leg
+            cpu = cpu_baseline(host_cpu_share(), nb, eps, args.test_mode)
         result = {
             "metric": f"Gnode-updates/s (nodes*steps/s) eps={eps} fp64",
             "value": value,
             "unit": "Gnode-updates/s",
             "n_gpus": nranks,
-            "nranks_seen": len(owned),
             "steps": args.steps,
             "warmup": args.warmup,
             "warmup_steps_run": warm,
@@ -463,11 +586,12 @@ def main() -> int:
                 "lattice": [nx, ny], "eps": eps, "blocks": [px, py], "test_mode": args.test_mode,
                 "disk_points": info.disk_points, "dt": dt, "dh": dh, "kernel": args.kernel,
                 "parallelism": f"{px}x{py} block decomposition, one rank per GPU" if nranks > 1 else "1 GPU",
+                "virtual_ranks": info.owners if nranks == 1 and info.owners > 1 else None,
             },
             "roofline": {
                 # contract: achieved = ALGORITHMIC bytes (16 B per
                 # node-update) per launch / average launch duration.  The two-step
-                # pass moves ~0.56x those bytes, so frac is an effective
+                # pass moves ~0.53x those bytes, so frac is an effective
                 # bandwidth; the physical limits are in roofline.physical
                 "bound": "hbm",
                 "achieved": achieved_gbs,
@@ -488,6 +612,7 @@ def main() -> int:
             },
             "cpu_baseline": cpu,
         }
+        result.update(scaling_fields(nranks, args.strong, ms_per_step, t1, phases, comm_seen))
         if l2 is not None:
             result["config"]["l2_error"] = l2  # reference error_l2 at the final step
         print(json.dumps(result), flush=True)

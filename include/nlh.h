@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define NLH_ABI_VERSION 8
+#define NLH_ABI_VERSION 9
 
 enum nlh_status {
   NLH_OK = 0,
@@ -62,13 +62,15 @@ enum nlh_influence { NLH_INFLUENCE_CONSTANT = 0, NLH_INFLUENCE_LINEAR = 1 };
 /* Stencil implementation.  EXACT reproduces the reference's per-term
  * floating-point order bit for bit (4 ops per neighbour; ((J c)(u_j - u_i))
  * dh^2 with J from a per-offset table when J != 1).  FAST computes the
- * same J=1 disk sum by nested (eps <= 16, 36..48) or prefix-sum (17..35 and,
- * with a run-time horizon in two passes, 49..64) row windows (~4*eps adds
- * per node) and, in test
- * mode, the manufactured source from a precomputed L_h[W0] field; it differs
- * from the reference only by summation rounding (<= 1e-12 of field scale per
- * node, L2 error within 1e-10).  AUTO = FAST wherever it is instantiated
- * (production and test mode), EXACT otherwise.                            */
+ * same J=1 disk sum from row windows, O(eps) adds per node instead of the
+ * N(eps) terms: nested windows for eps 1..16 (two-step k_pair_split, k_fast)
+ * and 36..64 (compile-time k_wide instances), prefix-sum windows for 17..35
+ * (k_wide), and past 64 a run-time-horizon prefix-window kernel (k_prefix_rt);
+ * in test mode the manufactured source comes from a precomputed L_h[W0]
+ * field.  FAST differs from the reference only by summation rounding
+ * (<= 1e-12 of field scale per node, L2 error within 1e-10).  AUTO = FAST
+ * (production and test mode), EXACT when FAST cannot apply (k*dt*dh = 0
+ * past eps 16).                                                           */
 enum nlh_kernel { NLH_KERNEL_AUTO = 0, NLH_KERNEL_EXACT = 1, NLH_KERNEL_FAST = 2 };
 
 typedef struct nlh_params {
@@ -165,6 +167,11 @@ typedef struct nlh_info {
                               or "k_exact"                                 */
   int32_t owners;          /* owner ids in the tile map: nranks, or the
                               NLH_VIRTUAL_RANKS count (nlh_rebalance sizes) */
+  int32_t comm_nranks;     /* ranks of the RCCL communicator as RCCL reports
+                              them (ncclCommCount; nlh_create fails when it
+                              differs from nranks), 0 without a communicator */
+  int32_t comm_rank;       /* this process's rank in it (ncclCommUserRank),
+                              -1 without a communicator                    */
   int32_t reserved_;
 } nlh_info;
 int nlh_get_info(const nlh_solver *s, nlh_info *info);
@@ -172,18 +179,43 @@ int nlh_get_info(const nlh_solver *s, nlh_info *info);
 /* Stencil-kernel timing with HIP events recorded on the stream the stencil
  * kernels are launched on.  enable == 1: every nlh_run call is bracketed by
  * one event pair on the interior stream (its passes run back to back in
- * between; a pass advances nlh_info.steps_per_pass time steps).  enable == 2
- * (busy time, the load balancer's input): an event pair around every stencil
- * launch group on the stream that runs it (interior and edge bands), so
- * halo waits are not counted -- the GPU counterpart of the reference's busy
- * rate, 10000 - idle-rate (src/2d_nonlocal_distributed.cpp:112-128,855-860).
- * The interior and band groups of a pass run concurrently on two streams and
- * both count, so busy time exceeds wall time where they overlap.  With
- * NLH_VIRTUAL_RANKS each virtual rank's launches are separate, each with its
- * own event pair.  nlh_kernel_time returns the summed duration and the
- * number of time steps advanced since the last enable.                     */
+ * between; a pass advances nlh_info.steps_per_pass time steps).
+ *
+ * enable == 2 (busy time, the load balancer's input; the GPU counterpart of
+ * the reference's busy rate, 10000 - idle-rate, src/2d_nonlocal_distributed.
+ * cpp:112-128,655-661,855-860): passes run serialised on one stream -- each
+ * (virtual) rank's edge bands, then each rank's interior, each launch group
+ * bracketed by its own event pair, the halo exchange of the next pass beside
+ * the interiors -- so a rank's busy time is the time its own kernels run,
+ * halo waits excluded, never more than the wall time, and under
+ * NLH_VIRTUAL_RANKS not inflated by the other ranks' kernels.  The launch
+ * overhead of an empty group (a no-op kernel between two events, measured
+ * when timing is enabled) is subtracted per launch.
+ *
+ * enable == 3 (phase timing, the multi-GPU overlap report): the normal
+ * schedule, with an event pair around every pass's interior group, edge-band
+ * group and halo exchange (pack, grouped send/recv, unpack) on the streams
+ * they run on, and one pair per nlh_run on the interior stream (wall);
+ * nlh_phase_time returns the sums.
+ *
+ * nlh_kernel_time returns the summed duration (modes 1 and 3: the per-run
+ * pairs; mode 2: every busy pair) and the number of time steps advanced
+ * since the last enable.                                                   */
 int nlh_kernel_timing(nlh_solver *s, int enable);
 int nlh_kernel_time(nlh_solver *s, double *total_ms, int64_t *steps);
+
+/* Phase times since nlh_kernel_timing(s, 3), summed over the passes run:
+ * wall = the nlh_run calls on the interior stream; interior / band /
+ * exchange = the interior kernels, the edge-band kernels and the halo
+ * exchange.  wall - interior is the time the interior stream spent waiting
+ * for bands and exchange (the exposed exchange: zero when the exchange hides
+ * entirely behind the interior).                                          */
+typedef struct nlh_phase_times {
+  double wall_ms, interior_ms, band_ms, exchange_ms;
+  int64_t passes;  /* passes (stencil launch rounds) timed                 */
+  int64_t steps;   /* time steps those passes advanced                    */
+} nlh_phase_times;
+int nlh_phase_time(nlh_solver *s, nlh_phase_times *out);
 
 /* Host-only (no device work): the owner rank of each tile as resolved by the
  * library (reference locidx(), src/2d_nonlocal_distributed.cpp:105-110).  */

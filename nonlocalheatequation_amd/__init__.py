@@ -33,7 +33,7 @@ __all__ = [
     "KERNEL_AUTO", "KERNEL_EXACT", "KERNEL_FAST", "INFLUENCE_CONSTANT", "INFLUENCE_LINEAR", "NLHError", "Solver",
     "lib", "lib_path", "comm_unique_id", "resolve_owner", "halo_plan", "block_plan",
     "disk_count", "batch_tester", "BatchRow", "Solver1D", "batch_tester_1d", "balance_owner",
-    "partition_tiles", "exchange_plan", "build_id", "source_build_id",
+    "partition_tiles", "exchange_plan", "build_id", "source_build_id", "PhaseTimes",
 ]
 
 KERNEL_AUTO, KERNEL_EXACT, KERNEL_FAST = 0, 1, 2
@@ -73,7 +73,15 @@ class _Info(ctypes.Structure):
         ("npeers", ctypes.c_int32), ("owned_nodes", ctypes.c_int64), ("disk_points", ctypes.c_int64),
         ("halo_bytes_sent", ctypes.c_int64), ("device_bytes", ctypes.c_int64),
         ("arch", ctypes.c_char * 32), ("halo_width", ctypes.c_int32), ("steps_per_pass", ctypes.c_int32),
-        ("pass_kernel", ctypes.c_char * 32), ("owners", ctypes.c_int32), ("reserved_", ctypes.c_int32),
+        ("pass_kernel", ctypes.c_char * 32), ("owners", ctypes.c_int32), ("comm_nranks", ctypes.c_int32),
+        ("comm_rank", ctypes.c_int32), ("reserved_", ctypes.c_int32),
+    ]
+
+
+class _PhaseTimes(ctypes.Structure):
+    _fields_ = [
+        ("wall_ms", ctypes.c_double), ("interior_ms", ctypes.c_double), ("band_ms", ctypes.c_double),
+        ("exchange_ms", ctypes.c_double), ("passes", ctypes.c_int64), ("steps", ctypes.c_int64),
     ]
 
 
@@ -108,6 +116,7 @@ _SIGNATURES = {
     "nlh_kernel_timing": ([ctypes.c_void_p, ctypes.c_int], ctypes.c_int),
     "nlh_kernel_time": ([ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
                          ctypes.POINTER(ctypes.c_int64)], ctypes.c_int),
+    "nlh_phase_time": ([ctypes.c_void_p, ctypes.POINTER(_PhaseTimes)], ctypes.c_int),
     "nlh_resolve_owner": ([ctypes.c_int64, ctypes.c_int64, ctypes.c_int32,
                            ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)], ctypes.c_int),
     "nlh_halo_plan": ([ctypes.POINTER(_Params), ctypes.POINTER(ctypes.c_int64), ctypes.c_int64],
@@ -335,6 +344,25 @@ class Info:
     steps_per_pass: int = 1
     pass_kernel: str = ""
     owners: int = 1
+    comm_nranks: int = 0   # ranks of the RCCL communicator (ncclCommCount), 0 without one
+    comm_rank: int = -1    # this rank in it (ncclCommUserRank)
+
+
+@dataclass
+class PhaseTimes:
+    """nlh_phase_time: summed milliseconds of the timed passes."""
+    wall_ms: float
+    interior_ms: float
+    band_ms: float
+    exchange_ms: float
+    passes: int
+    steps: int
+
+    @property
+    def exposed_exchange_ms(self) -> float:
+        """Interior-stream time not spent in interior kernels: the waits for
+        bands and exchange that the interior did not hide."""
+        return max(0.0, self.wall_ms - self.interior_ms)
 
 
 class Solver:
@@ -464,12 +492,22 @@ class Solver:
         _check(lib().nlh_get_info(self._h, ctypes.byref(i)), "nlh_get_info")
         return Info(i.kernel, i.device, i.nblocks, i.npeers, i.owned_nodes, i.disk_points,
                     i.halo_bytes_sent, i.device_bytes, i.arch.decode(), i.halo_width, i.steps_per_pass,
-                    i.pass_kernel.decode(), i.owners)
+                    i.pass_kernel.decode(), i.owners, i.comm_nranks, i.comm_rank)
 
     def kernel_timing(self, enable) -> None:
-        """False/0 off; True/1 one event pair per run(); 2 busy time (every
-        stencil launch group, halo waits excluded: the balancer's input)."""
-        _check(lib().nlh_kernel_timing(self._h, 2 if enable == 2 else int(bool(enable))), "nlh_kernel_timing")
+        """False/0 off; True/1 one event pair per run(); 2 busy time (passes
+        serialised, every rank's stencil launch groups timed, halo waits
+        excluded: the balancer's input); 3 phase timing (see phase_time())."""
+        mode = enable if enable in (2, 3) and not isinstance(enable, bool) else int(bool(enable))
+        _check(lib().nlh_kernel_timing(self._h, mode), "nlh_kernel_timing")
+
+    def phase_time(self) -> PhaseTimes:
+        """Since kernel_timing(3): wall (the run() calls on the interior
+        stream), interior kernels, edge-band kernels and halo exchange, summed
+        over the passes run."""
+        t = _PhaseTimes()
+        _check(lib().nlh_phase_time(self._h, ctypes.byref(t)), "nlh_phase_time")
+        return PhaseTimes(t.wall_ms, t.interior_ms, t.band_ms, t.exchange_ms, t.passes, t.steps)
 
     def repartition(self, owner) -> None:
         """Collective: move tiles to a new tile -> rank map (index gx + gy*tx);

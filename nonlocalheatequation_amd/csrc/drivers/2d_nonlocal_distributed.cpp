@@ -40,7 +40,8 @@ struct Run {
 };
 
 // owners in the tile map: the ranks, or NLH_VIRTUAL_RANKS on one rank
-// (diagnostics: every owner on one GPU, busy time apportioned by tiles)
+// (diagnostics: every owner on one GPU, each one's busy time measured on its
+// own kernels -- nlh_kernel_timing mode 2 runs them one after another)
 static int owners_of(const RankEnv &re) {
   if (const char *v = std::getenv("NLH_VIRTUAL_RANKS"))
     if (re.nranks == 1 && std::atoi(v) > 1) return std::atoi(v);
@@ -207,11 +208,13 @@ int main(int argc, char **argv) {
     return die("nlh_run");
 
   if (lb_test) {
-    // busy rate in the reference's units (10000 = busy the whole window):
-    // stencil time since the last rebalance over that window's wall time.
-    // Not clamped: interior and edge bands run on two streams at once and
-    // both count (nlh.h, nlh_kernel_timing), so a rate above 10000 shows that
-    // overlap instead of hiding it
+    // busy rate in the reference's units (10000 = busy the whole window,
+    // :655-661): stencil time since the last rebalance over that window's
+    // wall time.  Busy timing serialises each pass's kernels on one stream
+    // (nlh.h, nlh_kernel_timing mode 2), so the rate stays within
+    // [0, 10000] as the reference's 10000 - idle-rate does; under
+    // NLH_VIRTUAL_RANKS the owners share one GPU and the rates sum to at most
+    // 10000
     const double window_ms = std::max(1e-9, (now_ns() - window0) / 1e6);
     const int rc = nlh_rebalance(s, nullptr, 0, map.data(), busy.data());
     if (rc < 0) return die("nlh_rebalance");

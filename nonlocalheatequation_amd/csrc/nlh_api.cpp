@@ -229,6 +229,15 @@ struct Flag {
 
 constexpr size_t kEvFold = 4096;  // timing events kept before folding (nlh_run)
 
+// what one timing event pair brackets
+enum EvKind : int8_t { kEvRun = 0, kEvInterior = 1, kEvBand = 2, kEvExchange = 3 };
+struct EvMeta {
+  int32_t owner = -1;     // busy timing: the (virtual) rank of the launches
+  int16_t launches = 0;   // busy timing: kernel launches inside the pair
+  int8_t kind = kEvRun;
+  bool open = false;      // second event not recorded yet
+};
+
 struct Peer {
   int me = 0;     // the (virtual) rank of this process holding the buffers
   int rank = 0;   // the peer rank
@@ -297,17 +306,20 @@ struct nlh_solver {
   std::vector<int> part_off;
   int part_total = 0;
   double *d_red = nullptr;
-  // timing: 0 off, 1 one event pair per nlh_run, 2 busy (a pair per launch group)
+  // timing: 0 off, 1 one event pair per nlh_run, 2 busy (serialised passes, a
+  // pair per (virtual) rank's launch group), 3 phases (a pair per pass's
+  // interior, bands and exchange, one per nlh_run)
   int timing = 0;
-  std::vector<hipEvent_t> ev_pool;
+  std::vector<hipEvent_t> ev_pool;  // pair p = events 2p, 2p + 1
   size_t ev_used = 0;
-  std::vector<int> ev_steps;  // time steps covered by each timed event pair
-  std::vector<int> ev_owner;  // busy timing: the (virtual) rank of each event pair
-  // pairs already folded into a running total (long busy windows: the pool
-  // is drained every kEvFold events instead of growing with the run)
-  double ev_acc_ms = 0.0;
-  int64_t ev_acc_steps = 0;
+  std::vector<EvMeta> ev_meta;      // one per recorded pair
+  // pairs already folded into running totals (long windows: completed pairs
+  // are folded every kEvFold events instead of the pool growing with the run)
+  double ev_acc_kind[4] = {0.0, 0.0, 0.0, 0.0};  // per EvKind
   std::vector<double> ev_acc_owner;  // folded busy milliseconds per owner
+  int64_t timed_steps = 0, timed_passes = 0;  // since timing was enabled
+  double launch_overhead_ms = 0.0;  // busy timing: an empty launch between two events
+  int32_t comm_nranks = 0, comm_rank = -1;  // as RCCL reports them
   int64_t device_bytes = 0;
   char arch[32] = {0};
   // logging snapshots (nlh_snapshot_begin / _wait): owned nodes packed block
@@ -629,6 +641,36 @@ hipEvent_t pool_event(nlh_solver *s) {
   return s->ev_pool[s->ev_used++];
 }
 
+// a timed event pair: begin() records its first event on `st` and its
+// bookkeeping (open until end() records the second event; a fold inside
+// nlh_run keeps open pairs -- the per-run pair -- in flight)
+struct TimedPair {
+  nlh_solver *s;
+  hipEvent_t e1 = nullptr;
+  int begin(hipStream_t st, EvKind kind, int owner = -1, int launches = 0) {
+    hipEvent_t e0 = pool_event(s);
+    e1 = pool_event(s);
+    if (!e0 || !e1) return fail(NLH_ERR_HIP, "event pool");
+    HIP_TRY(hipEventRecord(e0, st));
+    EvMeta m;
+    m.kind = kind;
+    m.owner = owner;
+    m.launches = (int16_t)std::min(launches, 32767);
+    m.open = true;
+    s->ev_meta.push_back(m);
+    return NLH_OK;
+  }
+  int end(hipStream_t st) {
+    HIP_TRY(hipEventRecord(e1, st));
+    for (size_t p = s->ev_meta.size(); p-- > 0;)  // folds may have moved the pair
+      if (s->ev_pool[2 * p + 1] == e1) {
+        s->ev_meta[p].open = false;
+        return NLH_OK;
+      }
+    return fail(NLH_ERR_STATE, "internal: timing pair lost");
+  }
+};
+
 using RLIter = std::vector<nlh::RectList>::const_iterator;
 
 int launch_stencil(nlh_solver *s, RLIter b, RLIter e, hipStream_t st) {
@@ -706,6 +748,15 @@ int enqueue_exchange(nlh_solver *s, int k) {
   return NLH_OK;
 }
 
+// a pass's exchange; with phase timing (3) bracketed by its own event pair
+int enqueue_exchange_timed(nlh_solver *s, int k) {
+  if (s->timing != 3) return enqueue_exchange(s, k);
+  TimedPair tp{s};
+  int rc;
+  if ((rc = tp.begin(s->s_comm, kEvExchange)) || (rc = enqueue_exchange(s, k))) return rc;
+  return tp.end(s->s_comm);
+}
+
 // one time step (nsteps == 1, k_exact / k_fast) or two (nsteps == 2, the pair
 // kernel).  With an exchange (several blocks / ranks), pass n runs
 //   s_band : wait halo(n) and interior(n-1); bands(n)    (nodes within the
@@ -720,30 +771,36 @@ int enqueue_step(nlh_solver *s, int nsteps) {
   const int k = s->cur;
   const bool two = nsteps == 2;
   set_time(s, s->t);
+  if (s->timing) {
+    s->timed_steps += nsteps;
+    ++s->timed_passes;
+  }
+  // one group of stencil launches (interior, bands or the full block) on st
   auto stencil = [&](const std::vector<nlh::RectList> &one, const std::vector<nlh::RectList> &pr,
-                     hipStream_t st) {
+                     hipStream_t st, EvKind kind) {
     const std::vector<nlh::RectList> &v = two ? pr : one;
     auto run = [&](RLIter b, RLIter e) {
       return two ? launch_pair_lists(s, b, e, st) : launch_stencil(s, b, e, st);
     };
+    bool any = false;
+    for (const auto &rl : v) any |= rl.nwork > 0;
+    if (s->timing == 3 && any) {  // phase timing: one pair around the group
+      TimedPair tp{s};
+      int r;
+      if ((r = tp.begin(st, kind)) || (r = run(v.begin(), v.end()))) return r;
+      return tp.end(st);
+    }
     if (s->timing != 2) return run(v.begin(), v.end());
     // busy time: an event pair around each (virtual) rank's launches of this
-    // group (its lists are contiguous, build_rectlists); time steps are
-    // counted once, on the interior stream's first pair
-    bool first = true;
+    // group (its lists are contiguous, build_rectlists)
     for (RLIter b = v.begin(); b != v.end();) {
       RLIter e = b;
-      bool any = false;
-      while (e != v.end() && e->owner == b->owner) any |= (e++)->nwork > 0;
-      if (any) {
-        hipEvent_t e0 = pool_event(s), e1 = pool_event(s);
-        if (!e0 || !e1) return fail(NLH_ERR_HIP, "event pool");
-        HIP_TRY(hipEventRecord(e0, st));
-        if (const int r = run(b, e)) return r;
-        HIP_TRY(hipEventRecord(e1, st));
-        s->ev_steps.push_back(st == s->s_main && first ? nsteps : 0);
-        s->ev_owner.push_back(b->owner);
-        first = false;
+      int launches = 0;
+      while (e != v.end() && e->owner == b->owner) launches += (e++)->nwork > 0;
+      if (launches) {
+        TimedPair tp{s};
+        int r;
+        if ((r = tp.begin(st, kind, b->owner, launches)) || (r = run(b, e)) || (r = tp.end(st))) return r;
       }
       b = e;
     }
@@ -751,7 +808,7 @@ int enqueue_step(nlh_solver *s, int nsteps) {
   };
   int rc;
   if (!s->exchange) {
-    if ((rc = stencil(s->rl_full[k], s->pl_full[k], s->s_main))) return rc;
+    if ((rc = stencil(s->rl_full[k], s->pl_full[k], s->s_main, kEvInterior))) return rc;
   } else {
     if (!s->halo_fresh) {  // first pass after test_init / set_field: this input's halo
       HIP_TRY(hipEventRecord(s->ev_ready, s->s_main));
@@ -759,13 +816,25 @@ int enqueue_step(nlh_solver *s, int nsteps) {
       if ((rc = enqueue_exchange(s, k))) return rc;
       s->halo_fresh = true;
     }
-    if (s->sched == 1) {
+    if (s->timing == 2) {
+      // busy timing: the pass serialised on s_main -- halo(n), every rank's
+      // bands, every rank's interior -- so each rank's pairs time its own
+      // kernels alone (not the other ranks' kernels running beside them on a
+      // second stream) and no halo wait; the exchange of pass n + 1 runs on
+      // s_comm beside the interiors
+      HIP_TRY(hipStreamWaitEvent(s->s_main, s->ev_halo, 0));  // halo(n)
+      if ((rc = stencil(s->rl_bnd[k], s->pl_bnd[k], s->s_main, kEvBand))) return rc;
+      HIP_TRY(hipEventRecord(s->ev_band, s->s_main));
+      if ((rc = stencil(s->rl_int[k], s->pl_int[k], s->s_main, kEvInterior))) return rc;
+      HIP_TRY(hipEventRecord(s->ev_int, s->s_main));
+    } else if (s->sched == 1) {
       // bands(n) then interior(n), both on s_main: the bands run alone
       // briefly and the interior keeps its one-round grid
       HIP_TRY(hipStreamWaitEvent(s->s_main, s->ev_halo, 0));  // halo(n)
-      if ((rc = stencil(s->rl_bnd[k], s->pl_bnd[k], s->s_main))) return rc;
+      if ((rc = stencil(s->rl_bnd[k], s->pl_bnd[k], s->s_main, kEvBand))) return rc;
       HIP_TRY(hipEventRecord(s->ev_band, s->s_main));
-      if ((rc = stencil(s->rl_int[k], s->pl_int[k], s->s_main))) return rc;
+      if ((rc = stencil(s->rl_int[k], s->pl_int[k], s->s_main, kEvInterior))) return rc;
+      HIP_TRY(hipEventRecord(s->ev_int, s->s_main));
     } else if (s->sched == 2) {
       // bands(n) on the exchange stream, right before the exchange they feed:
       // the chain bands -> pack -> send/recv -> unpack -> next bands crosses
@@ -773,11 +842,11 @@ int enqueue_step(nlh_solver *s, int nsteps) {
       // do (about 11 us per cross-queue wait, profiles/r01/sched)
       HIP_TRY(hipStreamWaitEvent(s->s_main, s->ev_band, 0));  // bands(n-1)
       HIP_TRY(hipStreamWaitEvent(s->s_comm, s->ev_int, 0));   // interior(n-1)
-      if ((rc = stencil(s->rl_int[k], s->pl_int[k], s->s_main))) return rc;
+      if ((rc = stencil(s->rl_int[k], s->pl_int[k], s->s_main, kEvInterior))) return rc;
       HIP_TRY(hipEventRecord(s->ev_int, s->s_main));
-      if ((rc = stencil(s->rl_bnd[k], s->pl_bnd[k], s->s_comm))) return rc;
+      if ((rc = stencil(s->rl_bnd[k], s->pl_bnd[k], s->s_comm, kEvBand))) return rc;
       HIP_TRY(hipEventRecord(s->ev_band, s->s_comm));
-      if ((rc = enqueue_exchange(s, 1 - k))) return rc;
+      if ((rc = enqueue_exchange_timed(s, 1 - k))) return rc;
       s->cur = 1 - k;
       s->t += nsteps;
       return NLH_OK;
@@ -785,13 +854,13 @@ int enqueue_step(nlh_solver *s, int nsteps) {
       HIP_TRY(hipStreamWaitEvent(s->s_main, s->ev_band, 0));  // bands(n-1)
       HIP_TRY(hipStreamWaitEvent(s->s_band, s->ev_int, 0));   // interior(n-1)
       HIP_TRY(hipStreamWaitEvent(s->s_band, s->ev_halo, 0));  // halo(n)
-      if ((rc = stencil(s->rl_int[k], s->pl_int[k], s->s_main))) return rc;
+      if ((rc = stencil(s->rl_int[k], s->pl_int[k], s->s_main, kEvInterior))) return rc;
       HIP_TRY(hipEventRecord(s->ev_int, s->s_main));
-      if ((rc = stencil(s->rl_bnd[k], s->pl_bnd[k], s->s_band))) return rc;
+      if ((rc = stencil(s->rl_bnd[k], s->pl_bnd[k], s->s_band, kEvBand))) return rc;
       HIP_TRY(hipEventRecord(s->ev_band, s->s_band));
     }
     HIP_TRY(hipStreamWaitEvent(s->s_comm, s->ev_band, 0));
-    if ((rc = enqueue_exchange(s, 1 - k))) return rc;
+    if ((rc = enqueue_exchange_timed(s, 1 - k))) return rc;
   }
   s->cur = 1 - k;
   s->t += nsteps;
@@ -1075,6 +1144,20 @@ int create_impl(const nlh_params *pin, nlh_solver *s, ncclComm_t reuse_comm = nu
     NCCL_TRY(ncclGetUniqueId(&id));
     NCCL_TRY(ncclCommInitRank(&s->comm, 1, id, 0));
   }
+  if (s->comm) {
+    // the communicator's own view of the job: a real run must see every rank
+    // (a mis-launched job fails here instead of exchanging with the wrong peers)
+    int cn = 0, cr = -1;
+    NCCL_TRY(ncclCommCount(s->comm, &cn));
+    NCCL_TRY(ncclCommUserRank(s->comm, &cr));
+    s->comm_nranks = cn;
+    s->comm_rank = cr;
+    const int want_n = p.nranks > 1 ? (int)p.nranks : 1, want_r = p.nranks > 1 ? (int)p.rank : 0;
+    if (cn != want_n || cr != want_r)
+      return fail(NLH_ERR_RCCL, "RCCL communicator has " + std::to_string(cn) + " ranks (this one " +
+                                    std::to_string(cr) + "), expected " + std::to_string(want_n) + " (rank " +
+                                    std::to_string(want_r) + ")");
+  }
   rc = build_exchange(s);
   if (rc) return rc;
   if (s->exchange && !s->comm && !s->peers.empty())
@@ -1139,23 +1222,28 @@ int repartition_fits(nlh_solver *s, const std::vector<int32_t> &own) {
   const double scale = tiles_old > 0 ? (double)tiles_new / (double)tiles_old : 1.0;
   const double need = (double)s->device_bytes * scale * 1.05 + (double)(moving * tile_bytes) + 64.0 * (1 << 20);
   size_t free_b = 0, total_b = 0;
-  HIP_TRY(hipMemGetInfo(&free_b, &total_b));
-  int32_t ok = (double)free_b >= need ? 1 : 0;
+  // a local failure votes "does not fit" but still joins the all-reduce below:
+  // returning early here would leave the other ranks waiting in it
+  double ok = hipMemGetInfo(&free_b, &total_b) == hipSuccess && (double)free_b >= need ? 1.0 : 0.0;
   if (s->comm && !s->vranks && s->p.nranks > 1) {
-    int32_t *d = nullptr;
-    HIP_TRY(hipMalloc(&d, sizeof(int32_t)));
+    // the vote travels in the solver's own reduction scratch (d_red): the
+    // check allocates nothing
     int st = NLH_OK;
-    if (hipMemcpyAsync(d, &ok, sizeof(int32_t), hipMemcpyHostToDevice, s->s_comm) != hipSuccess)
+    if (hipMemcpyAsync(s->d_red, &ok, sizeof(double), hipMemcpyHostToDevice, s->s_comm) != hipSuccess) {
       st = fail(NLH_ERR_HIP, "repartition memory check upload");
-    if (st == NLH_OK && ncclAllReduce(d, d, 1, ncclInt32, ncclMin, s->comm, s->s_comm) != ncclSuccess)
+      ok = 0.0;
+    }
+    // every rank reaches this collective whatever happened above
+    if (ncclAllReduce(s->d_red, s->d_red, 1, ncclDouble, ncclMin, s->comm, s->s_comm) != ncclSuccess && st == NLH_OK)
       st = fail(NLH_ERR_RCCL, "repartition memory check all-reduce");
-    if (st == NLH_OK && hipMemcpyAsync(&ok, d, sizeof(int32_t), hipMemcpyDeviceToHost, s->s_comm) != hipSuccess)
+    double agreed = 0.0;
+    if (st == NLH_OK && hipMemcpyAsync(&agreed, s->d_red, sizeof(double), hipMemcpyDeviceToHost, s->s_comm) != hipSuccess)
       st = fail(NLH_ERR_HIP, "repartition memory check download");
     if (hipStreamSynchronize(s->s_comm) != hipSuccess && st == NLH_OK) st = fail(NLH_ERR_HIP, "repartition sync");
-    (void)hipFree(d);
     if (st) return st;
+    ok = agreed;
   }
-  if (!ok) {
+  if (ok < 1.0) {
     char buf[200];
     std::snprintf(buf, sizeof buf, "repartition needs ~%.0f MiB of device memory, %.0f MiB free (on this or another rank); "
                   "the solver is unchanged", need / (1 << 20), (double)free_b / (1 << 20));
@@ -1294,35 +1382,68 @@ int repartition_impl(nlh_solver *s, const std::vector<int32_t> &own) {
   n->cur = 0;
   n->halo_fresh = false;
   n->timing = s->timing;
+  n->launch_overhead_ms = s->launch_overhead_ms;
   release_impl(s, true);  // the communicator lives on in n
   *s = std::move(*n);
   delete n;  // moved-from shell: its resources now belong to s
   return NLH_OK;
 }
 
-// sum the recorded event pairs into the running total and recycle the pool
-int fold_events(nlh_solver *s) {
-  HIP_TRY(hipStreamSynchronize(s->s_main));
-  HIP_TRY(hipStreamSynchronize(s->s_comm));
-  HIP_TRY(hipStreamSynchronize(s->s_band));
-  for (size_t i = 0; i + 1 < s->ev_used; i += 2) {
-    float ms = 0.f;
-    HIP_TRY(hipEventElapsedTime(&ms, s->ev_pool[i], s->ev_pool[i + 1]));
-    s->ev_acc_ms += ms;
-    const int own = s->ev_owner[i / 2];
-    if (own >= 0 && own < (int)s->ev_acc_owner.size()) s->ev_acc_owner[own] += ms;
+// one completed pair into the running totals; busy pairs lose the measured
+// empty-launch overhead of each launch they bracket
+int fold_pair(nlh_solver *s, size_t p) {
+  float ms = 0.f;
+  HIP_TRY(hipEventElapsedTime(&ms, s->ev_pool[2 * p], s->ev_pool[2 * p + 1]));
+  const EvMeta &m = s->ev_meta[p];
+  double v = ms;
+  if (m.launches > 0) v = std::max(0.0, v - m.launches * s->launch_overhead_ms);
+  s->ev_acc_kind[m.kind] += v;
+  if (m.owner >= 0 && m.owner < (int)s->ev_acc_owner.size()) s->ev_acc_owner[m.owner] += v;
+  return NLH_OK;
+}
+
+// Fold recorded event pairs into the running totals and recycle their events.
+// drain: wait for every stream first and fold all.  Otherwise (the pool is
+// full inside a long run) wait only until the older half of the pairs has
+// completed and fold the pairs that have, keeping the rest in flight: the
+// host does not drain the GPU's queue.
+int fold_events(nlh_solver *s, bool drain) {
+  const size_t npairs = s->ev_meta.size();
+  if (drain) {
+    HIP_TRY(hipStreamSynchronize(s->s_main));
+    HIP_TRY(hipStreamSynchronize(s->s_comm));
+    HIP_TRY(hipStreamSynchronize(s->s_band));
+  } else if (npairs > 0) {
+    // the newest closed pair of the older half
+    for (size_t p = npairs / 2 + 1; p-- > 0;)
+      if (!s->ev_meta[p].open) {
+        HIP_TRY(hipEventSynchronize(s->ev_pool[2 * p + 1]));
+        break;
+      }
   }
-  for (int n : s->ev_steps) s->ev_acc_steps += n;
-  s->ev_used = 0;
-  s->ev_steps.clear();
-  s->ev_owner.clear();
+  size_t keep = 0;
+  for (size_t p = 0; p < npairs; ++p) {
+    if (s->ev_meta[p].open || !drain) {
+      const hipError_t q = s->ev_meta[p].open ? hipErrorNotReady : hipEventQuery(s->ev_pool[2 * p + 1]);
+      if (q == hipErrorNotReady) {  // still running (or open): move it to the front, fold later
+        std::swap(s->ev_pool[2 * keep], s->ev_pool[2 * p]);
+        std::swap(s->ev_pool[2 * keep + 1], s->ev_pool[2 * p + 1]);
+        s->ev_meta[keep++] = s->ev_meta[p];
+        continue;
+      }
+      if (q != hipSuccess) return fail(NLH_ERR_HIP, std::string("hipEventQuery: ") + hipGetErrorString(q));
+    }
+    if (int rc = fold_pair(s, p)) return rc;
+  }
+  s->ev_used = 2 * keep;
+  s->ev_meta.resize(keep);
   return NLH_OK;
 }
 
 // busy milliseconds of each (virtual) rank this process runs since busy
 // timing was enabled (index = rank; ranks run elsewhere stay 0)
 int owner_busy(nlh_solver *s, std::vector<double> &ms) {
-  if (int rc = fold_events(s)) return rc;
+  if (int rc = fold_events(s, true)) return rc;
   ms = s->ev_acc_owner;
   return NLH_OK;
 }
@@ -1555,31 +1676,24 @@ int nlh_run(nlh_solver *s, int64_t nsteps) {
   int rc = set_device(s);
   if (rc) return rc;
   if (nsteps == 0) return NLH_OK;
-  if (s->timing != 0 && s->ev_used >= kEvFold && (rc = fold_events(s))) return rc;
-  // timing: one event pair on the stencil stream around the whole call, so
-  // back-to-back passes are not separated by per-launch event records
-  hipEvent_t e0 = nullptr, e1 = nullptr;
-  if (s->timing == 1) {
-    e0 = pool_event(s);
-    e1 = pool_event(s);
-    if (!e0 || !e1) return fail(NLH_ERR_HIP, "event pool");
-    HIP_TRY(hipEventRecord(e0, s->s_main));
-  }
+  if (s->timing != 0 && s->ev_used >= kEvFold && (rc = fold_events(s, false))) return rc;
+  // timing 1 / 3: one event pair on the stencil stream around the whole call,
+  // so back-to-back passes are not separated by per-launch event records
+  TimedPair run_pair{s};
+  const bool per_run = s->timing == 1 || s->timing == 3;
+  if (per_run && (rc = run_pair.begin(s->s_main, kEvRun))) return rc;
   int64_t i = 0;
-  // busy timing records 2-4 event pairs per pass: fold them every kEvFold
-  // events inside one long call too, so the pool stays bounded
-  auto fold = [&] { return s->timing == 2 && s->ev_used >= kEvFold ? fold_events(s) : (int)NLH_OK; };
+  // busy and phase timing record 2-4 event pairs per pass: fold the completed
+  // ones every kEvFold events inside one long call too, so the pool stays
+  // bounded
+  auto fold = [&] { return s->timing >= 2 && s->ev_used >= kEvFold ? fold_events(s, false) : (int)NLH_OK; };
   if (s->pair)
     for (; i + 2 <= nsteps; i += 2)
       if ((rc = enqueue_step(s, 2)) || (rc = fold())) return rc;
   for (; i < nsteps; ++i)
     if ((rc = enqueue_step(s, 1)) || (rc = fold())) return rc;
   if (s->exchange) HIP_TRY(hipStreamWaitEvent(s->s_main, s->ev_band, 0));  // last bands
-  if (e1) {
-    HIP_TRY(hipEventRecord(e1, s->s_main));
-    s->ev_steps.push_back((int)nsteps);
-    s->ev_owner.push_back(-1);
-  }
+  if (per_run && (rc = run_pair.end(s->s_main))) return rc;
   return NLH_OK;
 }
 
@@ -1663,6 +1777,8 @@ int nlh_get_info(const nlh_solver *s, nlh_info *info) {
   info->halo_width = s->halo;
   info->steps_per_pass = s->pair ? 2 : 1;
   info->owners = s->owners;
+  info->comm_nranks = s->comm_nranks;
+  info->comm_rank = s->comm_rank;
   const char *pk = s->pair ? "k_pair_split"
                            : s->wide ? "k_wide" : s->weighted ? "k_weighted"
                            : s->kernel == NLH_KERNEL_FAST ? "k_fast"
@@ -1679,13 +1795,34 @@ int nlh_kernel_timing(nlh_solver *s, int enable) {
   HIP_TRY(hipStreamSynchronize(s->s_main));
   HIP_TRY(hipStreamSynchronize(s->s_comm));
   HIP_TRY(hipStreamSynchronize(s->s_band));
-  s->timing = enable == 2 ? 2 : enable != 0 ? 1 : 0;
+  s->timing = (enable == 2 || enable == 3) ? enable : enable != 0 ? 1 : 0;
   s->ev_used = 0;
-  s->ev_steps.clear();
-  s->ev_owner.clear();
-  s->ev_acc_ms = 0.0;
-  s->ev_acc_steps = 0;
+  s->ev_meta.clear();
+  for (double &v : s->ev_acc_kind) v = 0.0;
+  s->timed_steps = 0;
+  s->timed_passes = 0;
   s->ev_acc_owner.assign(s->owners, 0.0);
+  if (s->timing == 2) {
+    // the fixed cost of one launch between two events (an empty workgroup),
+    // the least of a few tries: subtracted per launch from the busy pairs
+    constexpr int kTries = 8;
+    for (int i = 0; i < kTries; ++i) {
+      const hipEvent_t e0 = pool_event(s), e1 = pool_event(s);
+      if (!e0 || !e1) return fail(NLH_ERR_HIP, "event pool");
+      HIP_TRY(hipEventRecord(e0, s->s_main));
+      if (nlh::launch_noop(s->s_main)) return fail(NLH_ERR_HIP, "no-op launch");
+      HIP_TRY(hipEventRecord(e1, s->s_main));
+    }
+    HIP_TRY(hipStreamSynchronize(s->s_main));
+    float best = 0.f;
+    for (int i = 0; i < kTries; ++i) {
+      float ms = 0.f;
+      HIP_TRY(hipEventElapsedTime(&ms, s->ev_pool[2 * i], s->ev_pool[2 * i + 1]));
+      best = i == 0 ? ms : std::min(best, ms);
+    }
+    s->launch_overhead_ms = std::max(0.f, best);
+    s->ev_used = 0;
+  }
   return NLH_OK;
 }
 
@@ -1696,16 +1833,30 @@ int nlh_kernel_time(nlh_solver *s, double *total_ms, int64_t *steps_out) {
   HIP_TRY(hipStreamSynchronize(s->s_main));
   HIP_TRY(hipStreamSynchronize(s->s_comm));
   HIP_TRY(hipStreamSynchronize(s->s_band));
-  double tot = s->ev_acc_ms;
-  for (size_t i = 0; i + 1 < s->ev_used; i += 2) {
-    float ms = 0.f;
-    HIP_TRY(hipEventElapsedTime(&ms, s->ev_pool[i], s->ev_pool[i + 1]));
-    tot += ms;
+  if ((rc = fold_events(s, true))) return rc;
+  if (s->timing == 2) {
+    double tot = 0.0;
+    for (double v : s->ev_acc_kind) tot += v;
+    *total_ms = tot;
+  } else {
+    *total_ms = s->ev_acc_kind[kEvRun];
   }
-  *total_ms = tot;
-  int64_t steps = s->ev_acc_steps;
-  for (int n : s->ev_steps) steps += n;
-  *steps_out = steps;
+  *steps_out = s->timed_steps;
+  return NLH_OK;
+}
+
+int nlh_phase_time(nlh_solver *s, nlh_phase_times *out) {
+  if (!s || !out) return fail(NLH_ERR_ARG, "null argument");
+  if (s->timing != 3) return fail(NLH_ERR_STATE, "phase timing is off (nlh_kernel_timing(s, 3))");
+  int rc = set_device(s);
+  if (rc) return rc;
+  if ((rc = fold_events(s, true))) return rc;
+  out->wall_ms = s->ev_acc_kind[kEvRun];
+  out->interior_ms = s->ev_acc_kind[kEvInterior];
+  out->band_ms = s->ev_acc_kind[kEvBand];
+  out->exchange_ms = s->ev_acc_kind[kEvExchange];
+  out->passes = s->timed_passes;
+  out->steps = s->timed_steps;
   return NLH_OK;
 }
 

@@ -121,6 +121,7 @@ int launch_weighted(const RectList &rl, const StepConst &c, bool test, void *str
 // A = sum_local(u) only (no time update) -- used once for L_h[W0].
 int launch_exact_sum(const RectList &rl, const StepConst &c, void *stream);
 int launch_copies(const CopyList &cl, void *stream);
+int launch_noop(void *stream);  // one empty workgroup (launch-overhead probe)
 // u(x,y) = sxt[gx]*syt[gy] on the block interior; halo untouched.
 int launch_init_test(double *u, int64_t pitch, int32_t bx, int32_t by,
                      int32_t gx0, int32_t gy0, const StepConst &c, void *stream);

@@ -37,3 +37,28 @@ def test_world_size_mismatch_is_an_error():
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1"],
                        env=env, capture_output=True, text=True, timeout=240, cwd=ROOT)
     assert p.returncode == 2 and "WORLD_SIZE" in p.stderr
+
+
+def test_multi_gpu_line_fields():
+    """The N > 1 line carries RCCL's own rank count, the per-pass exchange
+    report (max over ranks) and, with --strong, T1 / (N T_N)."""
+    phases = {"wall_ms": 100.0, "interior_ms": 80.0, "band_ms": 12.0, "exchange_ms": 30.0,
+              "exposed_exchange_ms": 20.0, "passes": 50, "steps": 100, "halo_bytes_sent": 3_145_728}
+    t1 = {"ms_per_step": 16.0, "value": 67.1, "build_id": "x", "kernel_avg_us": 3200.0}
+    f = bench.scaling_fields(8, True, 2.5, t1=t1, phases=phases, comm_seen=8)
+    assert f["nranks_seen"] == 8
+    assert f["strong_efficiency"] == 16.0 / (8 * 2.5)
+    assert f["strong_reference"]["n_gpus"] == 1
+    ex = f["exchange"]
+    for k in ("wall_ms_per_pass", "interior_ms_per_pass", "band_ms_per_pass", "exchange_ms_per_pass",
+              "exposed_exchange_ms_per_pass", "exposed_share_of_pass", "passes_timed", "halo_bytes_sent_per_pass"):
+        assert k in ex, k
+    assert ex["exchange_ms_per_pass"] == 30.0 / 50 and ex["exposed_exchange_ms_per_pass"] == 20.0 / 50
+    assert ex["steps_per_pass"] == 2 and ex["exposed_share_of_pass"] == 0.2
+    # weak scaling: no strong fields; a failed 1-GPU reference is reported, not hidden
+    w = bench.scaling_fields(4, False, 2.5, phases=phases, comm_seen=4)
+    assert "strong_efficiency" not in w and w["nranks_seen"] == 4
+    bad = bench.scaling_fields(2, True, 2.5, t1={"error": "boom"}, comm_seen=2)
+    assert bad["strong_efficiency"] is None and bad["strong_reference"] == {"error": "boom"}
+    # one GPU without a communicator
+    assert bench.scaling_fields(1, False, 1.0) == {"nranks_seen": 1}

@@ -15,7 +15,6 @@
 #include <vector>
 
 #include "nlh_pair.h"
-#include "pair_split_r3.h"
 
 using namespace nlh;
 
@@ -84,20 +83,12 @@ int main(int argc, char **argv) {
   // wait, 128 no store, 256 no DMA, 512 nt stores, 1024 nt DMA; 452 = VALU
   // only (no LDS reads, no vmcnt waits, no stores, no DMA)
   std::vector<Variant> vs = {
-      {"r3_split_D8_B4", k_pair_split_r3<E, 8, 0, 4>, 128, 4, 128 - 2 * E},
-      {"rows_D8_B4", k_pair_split<E, 8, 0, 4>, 128, 4, 128 - 2 * E},
       {"rows_D4_B2", k_pair_split<E, 4, 0, 2>, 128, 4, 128 - 2 * E},
-      {"rows_D6_B2", k_pair_split<E, 6, 0, 2>, 128, 4, 128 - 2 * E},
-      {"rows_D4_B4", k_pair_split<E, 4, 0, 4>, 128, 4, 128 - 2 * E},
-      {"r3_split_D8_B4_b", k_pair_split_r3<E, 8, 0, 4>, 128, 4, 128 - 2 * E},
-      {"rows_D8_B4_b", k_pair_split<E, 8, 0, 4>, 128, 4, 128 - 2 * E},
+      {"rows_D8_B4", k_pair_split<E, 8, 0, 4>, 128, 4, 128 - 2 * E},
       {"rows_D4_B2_b", k_pair_split<E, 4, 0, 2>, 128, 4, 128 - 2 * E},
-      {"rows_D6_B2_b", k_pair_split<E, 6, 0, 2>, 128, 4, 128 - 2 * E},
-      {"rows_D4_B4_b", k_pair_split<E, 4, 0, 4>, 128, 4, 128 - 2 * E},
-      {"r3_split_D8_B4_c", k_pair_split_r3<E, 8, 0, 4>, 128, 4, 128 - 2 * E},
-      {"rows_D8_B4_c", k_pair_split<E, 8, 0, 4>, 128, 4, 128 - 2 * E},
-      {"rows_D4_B2_c", k_pair_split<E, 4, 0, 2>, 128, 4, 128 - 2 * E},
+      {"rows_D8_B4_b", k_pair_split<E, 8, 0, 4>, 128, 4, 128 - 2 * E},
   };
+
 
 
 
