@@ -26,7 +26,8 @@ BUILD_ID := $(shell cat $(BUILD_ID_SRCS) | sha256sum | cut -c1-16)
 
 FAST_UNITS := $(sort $(wildcard $(CSRC)/nlh_fast_e*.hip $(CSRC)/nlh_pair_e*.hip $(CSRC)/nlh_wide_e*.hip))
 FAST_OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(FAST_UNITS))
-LIB_OBJS := $(OBJDIR)/nlh_kernels.o $(FAST_OBJS) $(OBJDIR)/nlh_api.o $(OBJDIR)/nlh_plan.o $(OBJDIR)/nlh_1d.o
+LIB_OBJS := $(OBJDIR)/nlh_kernels.o $(FAST_OBJS) $(OBJDIR)/nlh_prefix.o $(OBJDIR)/nlh_api.o $(OBJDIR)/nlh_plan.o \
+            $(OBJDIR)/nlh_1d.o
 # the fast kernel is fully unrolled over 2E+1 rows; lift LLVM's pragma-unroll
 # size cap so every accumulator stays in registers (no scratch)
 UNROLL  := -mllvm -pragma-unroll-threshold=1000000
@@ -57,6 +58,9 @@ $(OBJDIR)/nlh_pair_%.o: $(CSRC)/nlh_pair_%.hip $(CHDRS) $(CSRC)/nlh_pair.h | $(O
 
 $(OBJDIR)/nlh_wide_%.o: $(CSRC)/nlh_wide_%.hip $(CHDRS) $(CSRC)/nlh_wide.h | $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) $(UNROLL) -c $< -o $@
+
+$(OBJDIR)/nlh_prefix.o: $(CSRC)/nlh_prefix.hip $(CHDRS) $(CSRC)/nlh_prefix.h $(CSRC)/nlh_rt.h | $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(OBJDIR)/nlh_api.o: $(CSRC)/nlh_api.cpp $(BUILD_ID_SRCS) | $(OBJDIR)
 	$(HIPCC) $(HOSTFLAGS) -DNLH_BUILD_ID='"$(BUILD_ID)"' -x c++ -c $< -o $@

@@ -30,6 +30,7 @@
 #include "nlh.h"
 #include "nlh_device.h"
 #include "nlh_plan.h"
+#include "nlh_rt.h"
 
 namespace {
 
@@ -77,6 +78,7 @@ struct Resolved {
   bool pair = false;  // two steps per pass (nlh_pair.h)
   bool wide = false;  // large-horizon single-step kernel (nlh_wide.h)
   bool weighted = false;  // non-constant J: k_weighted (fast) instead of the J = 1 kernels
+  bool prefix = false;  // run-time-horizon k_prefix_rt (eps past the k_wide instances)
   int halo = 0;       // eps, or 2*eps with pair
 };
 
@@ -101,7 +103,7 @@ int resolve_config(const nlh_params &p, Resolved &r) {
   // L2 within 1e-10 of the reference; EXACT remains selectable for bitwise
   // parity)
   if (kern == NLH_KERNEL_AUTO) kern = NLH_KERNEL_FAST;
-  if (kern == NLH_KERNEL_FAST && !nlh::fast_supported(E)) {
+  if (kern == NLH_KERNEL_FAST && !nlh::fast_supported(E) && !nlh::prefix_rt_supported(E)) {
     // beyond the nested-window horizons: the LDS-tile kernel with J = 1
     if (nlh::weighted_supported(E)) {
       r.kernel = kern;
@@ -115,14 +117,16 @@ int resolve_config(const nlh_params &p, Resolved &r) {
   }
   const double alpha = ((p.k * 8) / pow(p.eps * p.dh, 4)) * (p.dh * p.dh) * p.dt;
   const bool fold_ok = alpha != 0.0 && std::isfinite(1.0 / alpha);  // centre fold usable
-  if (kern == NLH_KERNEL_FAST && nlh::wide_supported(E) && !fold_ok) {
-    // the large-horizon kernel folds the centre term (1/alpha - N)
+  const bool folds = nlh::wide_supported(E) || nlh::prefix_rt_supported(E);
+  if (kern == NLH_KERNEL_FAST && folds && !fold_ok) {
+    // the large-horizon kernels fold the centre term (1/alpha - N)
     if (p.kernel == NLH_KERNEL_FAST)
       return fail(NLH_ERR_UNSUPPORTED, "fast kernel for eps > 16 needs k*dt*dh != 0");
     kern = NLH_KERNEL_EXACT;
   }
   r.kernel = kern;
   r.wide = kern == NLH_KERNEL_FAST && nlh::wide_supported(E);
+  r.prefix = kern == NLH_KERNEL_FAST && nlh::prefix_rt_supported(E);
   // fast mode advances two steps per pass (test mode too: the manufactured
   // source of both steps folded into the pass); a zero alpha (no centre fold)
   // keeps the single-step kernels
@@ -260,6 +264,8 @@ struct nlh_solver {
   bool pair = false;  // two steps per pass (nlh_pair.h); production fast mode (NLH_PAIR=0 disables)
   bool wide = false;  // k_wide (nlh_wide.h) for eps 17..48
   bool weighted = false;  // k_weighted: non-constant influence function
+  bool prefix = false;    // k_prefix_rt (nlh_prefix.h) past the k_wide horizons
+  int32_t *d_ptab = nullptr;  // k_prefix_rt's per-offset prefix index table
   double *d_wt = nullptr, *d_qj = nullptr;  // J tables (influence != 0)
   int halo = 0;       // halo rows/columns held per block: eps, or 2*eps with pair
   // production k_pair_split rings: 6 = D4/B2 (default; with row pairs 444-450 vs 438-446 G
@@ -438,6 +444,8 @@ int build_rectlists(nlh_solver *s, int kind) {
           if (seg == 16) break;
         }
         seg_h = own ? s->p.seg_rows : (int)best;
+      } else if (s->prefix) {
+        seg_h = nlh::kPrefixRows;  // the kernel's register block of output rows
       } else if (s->wide) {
         // k_wide: one-wave workgroups, all resident in one round: two waves per
         // SIMD up to E = 40 (8 per CU, 214 VGPRs at E = 32;
@@ -462,6 +470,7 @@ int build_rectlists(nlh_solver *s, int kind) {
       seg_band = (int)std::min<int64_t>(seg_h, std::max<int64_t>(lo, ceil_div(band_rows, (int64_t)s->cus)));
       if (const char *bsg = std::getenv("NLH_BAND_SEG"))
         if (std::atoi(bsg) > 0) seg_band = std::atoi(bsg);
+      if (s->prefix) seg_band = seg_h;  // fixed R-row blocks
     }
     return {seg_h, seg_band};
   };
@@ -681,6 +690,8 @@ int launch_stencil(nlh_solver *s, RLIter b, RLIter e, hipStream_t st) {
     int rc;
     if (s->weighted)
       rc = nlh::launch_weighted(rl, s->sc, test, st);
+    else if (s->prefix)
+      rc = nlh::launch_prefix_rt(rl, s->sc, s->d_ptab, test, st);
     else if (s->wide)
       rc = nlh::launch_wide(rl, s->sc, test, st);
     else if (s->kernel == NLH_KERNEL_FAST)
@@ -921,6 +932,7 @@ void release_impl(nlh_solver *s, bool keep_comm) {
   }
   (void)hipFree(s->d_wt);
   (void)hipFree(s->d_qj);
+  (void)hipFree(s->d_ptab);
   (void)hipFree(s->d_sxt);
   (void)hipFree(s->d_syt);
   (void)hipFree(s->d_lens);
@@ -999,6 +1011,7 @@ int create_impl(const nlh_params *pin, nlh_solver *s, ncclComm_t reuse_comm = nu
   s->pair = rv.pair;
   s->wide = rv.wide;
   s->weighted = rv.weighted;
+  s->prefix = rv.prefix;
   if (const char *fb = std::getenv("NLH_FORCE_BANDS")) s->force_bands = std::atoi(fb) != 0;
   if (const char *rs = std::getenv("NLH_RCCL_SELF")) s->rccl_self = p.nranks == 1 && std::atoi(rs) != 0;
   if (vranks) s->rccl_self = true;  // virtual owners talk over RCCL to self
@@ -1081,7 +1094,13 @@ int create_impl(const nlh_params *pin, nlh_solver *s, ncclComm_t reuse_comm = nu
   s->sc.dt = p.dt;
   s->sc.alpha = s->sc.c2d * s->sc.dh2 * p.dt;
   s->sc.nf = (double)s->disk;
-  s->sc.kc = (s->pair || s->wide) ? 1.0 / s->sc.alpha - s->sc.nf : 0.0;
+  s->sc.kc = (s->pair || s->wide || s->prefix) ? 1.0 / s->sc.alpha - s->sc.nf : 0.0;
+  if (s->prefix) {
+    std::vector<int32_t> tab(2 * (size_t)nlh::prefix_rt_table_size(E));
+    nlh::prefix_rt_table(E, lens.data(), tab.data());
+    HIP_TRY(hipMalloc(&s->d_ptab, tab.size() * sizeof(int32_t)));
+    HIP_TRY(hipMemcpy(s->d_ptab, tab.data(), tab.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+  }
   s->sc.sxt = s->d_sxt;
   s->sc.syt = s->d_syt;
   s->sc.lens = s->d_lens;
@@ -1104,7 +1123,9 @@ int create_impl(const nlh_params *pin, nlh_solver *s, ncclComm_t reuse_comm = nu
     b.xl = (int32_t)XL;
     // whole 256-column strips stay in bounds; the pair kernel's last strip
     // stages up to column w + 127
-    const int64_t right = std::max(round_up(b.r.w, 256) + XL, s->pair ? b.r.w + 128 : 0);
+    // (k_prefix_rt stages 64 NV <= 512 columns from x0 - E of its last strip)
+    const int64_t right = std::max({round_up(b.r.w, 256) + XL, s->pair ? b.r.w + 128 : (int64_t)0,
+                                    s->prefix ? round_up(b.r.w, 64) + 512 : (int64_t)0});
     b.pitch = round_up(XL + right, 8) + pitch_pad;
     b.rows = b.r.h + 2 * s->halo;
     b.L = b.r.x0 > 0 || s->force_bands;
@@ -1780,7 +1801,7 @@ int nlh_get_info(const nlh_solver *s, nlh_info *info) {
   info->comm_nranks = s->comm_nranks;
   info->comm_rank = s->comm_rank;
   const char *pk = s->pair ? "k_pair_split"
-                           : s->wide ? "k_wide" : s->weighted ? "k_weighted"
+                           : s->wide ? "k_wide" : s->prefix ? "k_prefix_rt" : s->weighted ? "k_weighted"
                            : s->kernel == NLH_KERNEL_FAST ? "k_fast"
                            : nlh::exact_lds_ok((int)s->p.eps, s->p.test != 0) ? "k_exact_lds" : "k_exact";
   std::snprintf(info->pass_kernel, sizeof(info->pass_kernel), "%s", pk);

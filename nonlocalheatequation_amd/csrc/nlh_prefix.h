@@ -1,0 +1,147 @@
+// nlh_prefix.h -- k_prefix_rt: single-step production / fast test-mode
+// kernel for horizons past the compile-time k_wide instances (eps > 64), the
+// horizon a run-time value.  Same operator as k_wide (reference sum_local,
+// src/2d_nonlocal_serial.cpp:256-270 with J = 1; update :279-284; the
+// reference accepts any --eps, :403):
+//
+//   S(x, y) = sum_{dy = -E..E} H_len(|dy|)(x, y + dy),
+//   H_L(x, r) = sum_{|dx| <= L} u(x + dx, r) = P_r(x + L) - P_r(x - L - 1),
+//
+// P_r the prefix sum of input row r.  One wave per work item: 64 output
+// columns (one per lane) x R output rows, accumulators in registers.  The
+// wave streams the 2E + R input rows the block needs; per row each lane loads
+// NV consecutive values of the staged window (64 + 2E <= 64 NV columns),
+// sums them, scans the lane totals over the wave (DPP) and writes the
+// prefix row to LDS; then every output row j of the block within the horizon
+// adds H_len(|d|) = P(c + L) - P(c - L - 1), d = r - (y0 + j): two LDS reads,
+// one subtraction, one add per (input row, output row) pair -- O(eps) per
+// node instead of the O(eps^2) terms of k_exact.
+//
+// The per-offset prefix indices (c + L and c - L - 1 relative to the lane's
+// centre, both 0 where |d| > E so the pair adds P(c) - P(c) = +0) come
+// from a host table indexed by d + E + R, read with uniform (scalar) loads,
+// so no pair branches.  Centre fold as k_wide: u' = alpha (S + (1/alpha - N)
+// u), u read back from the field at the store; the fast test-mode source
+// dt b enters as (dt/alpha) b with b = -(2 pi st) W0 - ct L_h[W0].
+//
+// The difference of two prefix sums of <= 64 NV values rounds at ~2^-44 of
+// the row's magnitude; alpha ~ 1/N(eps) scales the disk sum of 2E + 1 of
+// them, far inside the 1e-12 field-scale tolerance (tests/test_gpu_parity.py).
+#pragma once
+
+#include "nlh_device.h"
+#include "nlh_kernel_common.h"
+#include "nlh_rt.h"
+
+namespace nlh {
+
+// inclusive wave prefix sum (DPP row_shr 1/2/4/8, row_bcast 15/31), as k_wide
+__device__ __forceinline__ double rt_wave_prefix(double x) {
+  auto sh = [](double v, auto ctrl, auto rmask, auto bc) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), decltype(ctrl)::value,
+                                               decltype(rmask)::value, 0xf, decltype(bc)::value);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), decltype(ctrl)::value,
+                                               decltype(rmask)::value, 0xf, decltype(bc)::value);
+    return __hiloint2double(hi, lo);
+  };
+  x += sh(x, std::integral_constant<int, 0x111>{}, std::integral_constant<int, 0xf>{}, std::true_type{});
+  x += sh(x, std::integral_constant<int, 0x112>{}, std::integral_constant<int, 0xf>{}, std::true_type{});
+  x += sh(x, std::integral_constant<int, 0x114>{}, std::integral_constant<int, 0xf>{}, std::true_type{});
+  x += sh(x, std::integral_constant<int, 0x118>{}, std::integral_constant<int, 0xf>{}, std::true_type{});
+  x += sh(x, std::integral_constant<int, 0x142>{}, std::integral_constant<int, 0xa>{}, std::false_type{});
+  x += sh(x, std::integral_constant<int, 0x143>{}, std::integral_constant<int, 0xc>{}, std::false_type{});
+  return x;
+}
+
+// NV staged values per lane (window of 64 NV columns: 64 + 2 E rounded up
+// to even <= 64 NV),
+// R output rows per work item (seg_rows of the rect list)
+template <int NV, int R, bool TEST>
+__global__ __launch_bounds__(64) void k_prefix_rt(RectList L, StepConst C, const int2 *__restrict__ tab) {
+  constexpr int NPF = 64 * NV + 2;  // doubles per prefix slot: [0] = P(-1) = 0, [1 + k] = P(k)
+  __shared__ __attribute__((aligned(16))) double pf[2][NPF];
+  const int lane = (int)threadIdx.x;
+  const int E = C.E;
+  const int work = xcd_remap(blockIdx.x, gridDim.x);
+  const int ri = find_rect(L, work);
+  const Rect &Rc = L.r[ri];
+  const int local = work - Rc.wg_begin;
+  const int strip = local % Rc.nstrip, seg = local / Rc.nstrip;
+  const int x0 = Rc.x0 + strip * 64;
+  const int y0 = Rc.y0 + seg * Rc.seg_rows;
+  const int nout = min(R, Rc.y1 - y0);  // seg_rows == R (host)
+  const int64_t pitch = Rc.pitch;
+  const int xl = x0 + lane;
+  const bool emit = xl < Rc.x1;
+  if (lane == 0) {
+    pf[0][0] = 0.0;
+    pf[1][0] = 0.0;
+  }
+  // staged window: columns x0 - EP .. x0 - EP + 64 NV - 1 (EP = E rounded up
+  // to even: 16-byte aligned rows, each lane's NV values two dwordx4 loads).
+  // The columns past x0 + 63 + E feed no lane's window; they lie inside the
+  // block's right padding (nlh_api.cpp sizes it for this window)
+  const int EP = E + (E & 1);
+  const double *gcol = Rc.u + (x0 - EP + NV * lane);
+  auto load_row = [&](int r, double (&v)[NV]) __attribute__((always_inline)) {
+    const double2 *g = reinterpret_cast<const double2 *>(gcol + (int64_t)r * pitch);
+#pragma unroll
+    for (int k = 0; k < NV / 2; ++k) {
+      const double2 w = g[k];
+      v[2 * k] = w.x;
+      v[2 * k + 1] = w.y;
+    }
+  };
+  double acc[R];
+#pragma unroll
+  for (int j = 0; j < R; ++j) acc[j] = 0.0;
+
+  const int rfirst = y0 - E, rend = y0 + nout + E;  // input rows [rfirst, rend)
+  double cur[NV], nxt[NV];
+  load_row(rfirst, cur);
+  for (int r = rfirst; r < rend; ++r) {
+    const int s = (r - rfirst) & 1;
+    if (r + 1 < rend) load_row(r + 1, nxt);
+    // prefix row of input row r into slot s
+    double p[NV];
+    p[0] = cur[0];
+#pragma unroll
+    for (int k = 1; k < NV; ++k) p[k] = p[k - 1] + cur[k];
+    const double incl = rt_wave_prefix(p[NV - 1]);
+    const double ex = incl - p[NV - 1];
+    double *dst = &pf[s][1 + NV * lane];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) dst[k] = ex + p[k];
+    asm volatile("" ::: "memory");  // LDS is in order per wave: the reads below see every lane's write
+    // pairs: output j <- d = r - (y0 + j); table entry d + E + R
+    const int2 *t = tab + (r - y0 + E + R);
+    const double *cen = &pf[s][1 + EP + lane];  // the lane's P(c), c = EP + lane
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const int2 o = t[-j];  // {L, -L - 1}, or {0, 0} past the horizon
+      acc[j] += cen[o.x] - cen[o.y];
+    }
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int k = 0; k < NV; ++k) cur[k] = nxt[k];
+  }
+  // u' = alpha (S + kc u) [+ (dt/alpha) b]: u(x, y) from the field
+  const double alpha = C.alpha, kc = C.kc;
+  const double qs = TEST ? C.dt / alpha : 0.0;
+  const double sxv = TEST ? C.sxt[Rc.gx0 + min(xl, Rc.x1 - 1) + E] : 0.0;
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    if (j < nout && emit) {
+      const int64_t off = (int64_t)(y0 + j) * pitch + xl;
+      double a = fma(kc, Rc.u[off], acc[j]);
+      if constexpr (TEST) {
+        const double syv = C.syt[Rc.gy0 + y0 + j + E];
+        const double b = -(C.st2pi * (sxv * syv)) - C.ct * Rc.lw[off];
+        a = fma(qs, b, a);
+      }
+      Rc.un[off] = alpha * a;
+    }
+  }
+}
+
+}  // namespace nlh

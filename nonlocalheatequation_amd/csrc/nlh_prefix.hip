@@ -1,0 +1,35 @@
+// nlh_prefix.hip -- instances and launcher of k_prefix_rt (nlh_prefix.h).
+#include "nlh_prefix.h"
+
+namespace nlh {
+
+bool prefix_rt_supported(int E) { return E >= 65 && E <= 224; }
+
+int prefix_rt_table_size(int E) { return 2 * (E + kPrefixRows) + 1; }
+
+void prefix_rt_table(int E, const int32_t *lens, int32_t *out) {
+  for (int i = 0; i < prefix_rt_table_size(E); ++i) {
+    const int d = i - E - kPrefixRows;
+    const int ad = d < 0 ? -d : d;
+    out[2 * i] = ad <= E ? lens[ad] : 0;
+    out[2 * i + 1] = ad <= E ? -lens[ad] - 1 : 0;
+  }
+}
+
+template <int NV, bool TEST>
+static int launch_nv(const RectList &rl, const StepConst &c, const void *table, hipStream_t st) {
+  hipLaunchKernelGGL((k_prefix_rt<NV, kPrefixRows, TEST>), dim3(rl.nwork), dim3(64), 0, st, rl, c,
+                     (const int2 *)table);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : (int)e;
+}
+
+int launch_prefix_rt(const RectList &rl, const StepConst &c, const void *table, bool test, void *stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (rl.nwork <= 0) return 0;
+  if (c.E <= 96) return test ? launch_nv<4, true>(rl, c, table, st) : launch_nv<4, false>(rl, c, table, st);
+  if (c.E <= 224) return test ? launch_nv<8, true>(rl, c, table, st) : launch_nv<8, false>(rl, c, table, st);
+  return -1;
+}
+
+}  // namespace nlh

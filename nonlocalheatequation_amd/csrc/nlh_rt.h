@@ -1,0 +1,19 @@
+// nlh_rt.h -- host launch API of k_prefix_rt (nlh_prefix.h, nlh_prefix.hip):
+// the run-time-horizon kernel for eps past the compile-time k_wide instances.
+#pragma once
+#include <cstdint>
+
+#include "nlh_device.h"
+
+namespace nlh {
+
+constexpr int kPrefixRows = 32;  // R: output rows per work item (the rect lists' seg_rows)
+// horizons k_prefix_rt serves: 65 .. 224 (staged window 64 + 2E <= 512 columns)
+bool prefix_rt_supported(int E);
+// host table of 2 (E + R) + 1 int2 entries, index d + E + R: {L, -L - 1}
+// with L = len(|d|) for |d| <= E, {0, 0} beyond
+int prefix_rt_table_size(int E);
+void prefix_rt_table(int E, const int32_t *lens, int32_t *out);
+int launch_prefix_rt(const RectList &rl, const StepConst &c, const void *table, bool test, void *stream);
+
+}  // namespace nlh

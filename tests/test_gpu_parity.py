@@ -192,8 +192,63 @@ def test_large_eps_64_blocks(oracle, monkeypatch, eps, tiles):
     assert np.max(np.abs(u - ref)) <= 1e-12 * np.max(np.abs(ref))
 
 
-@pytest.mark.parametrize("eps", [65, 80])
+def _smooth_noisy_ic(nx, ny, dh, seed):
+    """sin sin + 1e-2 noise: at large horizons a field of pure noise shrinks
+    ~30x per few steps and the reference order's own rounding (N(eps) terms
+    summed in sequence) is then ~1e-12 of what is left; any indexing slip
+    still shows at alpha * 1e-2 >> 1e-12 (test_large_eps_64_blocks)."""
+    xs, ys = np.meshgrid(np.arange(nx) * dh, np.arange(ny) * dh)
+    return np.sin(2 * np.pi * xs) * np.sin(2 * np.pi * ys) + \
+        1e-2 * np.random.default_rng(seed).uniform(-1, 1, size=(ny, nx))
+
+
+@pytest.mark.parametrize("eps", [65, 71, 80, 96, 97, 130])
+@pytest.mark.parametrize("test", [False, True])
+def test_prefix_rt_vs_oracle(oracle, eps, test):
+    """eps past the k_wide instances (the reference accepts any --eps,
+    src/2d_nonlocal_serial.cpp:403): AUTO/FAST run k_prefix_rt (run-time
+    horizon, prefix-sum row windows; 4 staged values per lane to eps 96, 8
+    beyond), per node within 1e-12 of field scale, L2 by the recorded
+    criterion; EXACT stays bitwise.  Ragged lattice narrower than four strips,
+    shorter than two horizons, rows in 32-row blocks (the last partial)."""
+    nx, ny, nt = 200, 171, 3
+    dh = 1.0 / nx
+    r = N.BatchRow(nx, ny, nt, eps, 1.0, 0.5 * eps ** 4 * dh * dh / (8 * N.disk_count(eps)), dh)
+    u0 = None if test else _smooth_noisy_ic(nx, ny, dh, eps)
+    p = oracle.params(nx, ny, eps, r.k, r.dt, dh, int(test))
+    ref = oracle.run(p, nt, u0)
+    u, (l2, _), info = _gpu_run_j(r, test, "auto", "constant", u0)
+    assert info.pass_kernel == "k_prefix_rt" and info.kernel == N.KERNEL_FAST
+    assert np.max(np.abs(u - ref)) <= 1e-12 * np.max(np.abs(ref))
+    if test:
+        check_l2(l2, oracle.errors(p, nt, ref)[0], u, ref, f"k_prefix_rt eps {eps}")
+    ue, _, info = _gpu_run_j(r, test, "exact", "constant", u0)
+    assert info.kernel == N.KERNEL_EXACT and np.array_equal(ue, ref)
+
+
+@pytest.mark.parametrize("tiles", [(3, 2), (1, 4)])
+def test_prefix_rt_blocks(oracle, monkeypatch, tiles):
+    """k_prefix_rt at eps 80 through the multi-block exchange (RCCL to self),
+    blocks narrower / shorter than the horizon's window, vs the oracle."""
+    monkeypatch.setenv("NLH_RCCL_SELF", "1")
+    nx, ny, nt, eps = 240, 200, 3, 80
+    dh = 1.0 / nx
+    dt = 0.7 * eps ** 4 * dh * dh / (8 * N.disk_count(eps))
+    u0 = _smooth_noisy_ic(nx, ny, dh, 7)
+    ref = oracle.run(oracle.params(nx, ny, eps, 1.0, dt, dh, 0), nt, u0)
+    with N.Solver(nx, ny, eps, 1.0, dt, dh, kernel="fast", tiles=tiles, split_tiles=True) as s:
+        s.input_init(u0)
+        s.run(nt)
+        s.synchronize()
+        u = s.field()
+        assert s.info().pass_kernel == "k_prefix_rt" and s.info().nblocks == tiles[0] * tiles[1]
+    assert np.max(np.abs(u - ref)) <= 1e-12 * np.max(np.abs(ref))
+
+
+@pytest.mark.parametrize("eps", [225, 240])
 def test_unsupported_fast_eps_falls_back_to_exact(oracle, eps):
+    """Past k_prefix_rt's staged window (64 + 2 eps > 512 columns) AUTO runs
+    the exact kernel and an explicit FAST request is refused."""
     r = N.BatchRow(60, 50, 2, eps, 1.0, 1e-4, 1.0 / 60)
     with N.Solver(r.nx, r.ny, eps, r.k, r.dt, r.dh, test=False, kernel="auto") as s:
         assert s.info().kernel == N.KERNEL_EXACT

@@ -4,7 +4,7 @@
 #   2. smoke, the driver's 20-step C2 line
 #   3. C3 as 8 virtual ranks on one GPU (2x4 blocks of 16384x8192): bench line
 #      with the per-pass exchange report, and its rocprofv3 kernel trace
-#   4. eps 13 test mode: k_pair_split vs k_fast (NLH_PAIR=0); k_exact at eps 80 / 96
+#   4. eps 13 test mode: k_pair_split vs k_fast (NLH_PAIR=0); eps > 64: k_exact vs k_prefix_rt
 # Every GPU step under its own time limit; stops at the first failure.
 set -o pipefail
 export TMPDIR=/tmp
@@ -22,6 +22,9 @@ NLH_VIRTUAL_RANKS=8 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/c3_
 timeout -k 10 200 python bench.py --strong --lattice 32768 --steps 40 --pmc off --no-cpu-baseline > $O/c3_1block.json 2> $O/c3_1block.err || exit 1
 timeout -k 10 200 python bench.py --eps 13 --test-mode --steps 400 --pmc off --no-cpu-baseline > $O/eps13_test_pair.json 2> $O/eps13_test_pair.err || exit 1
 NLH_PAIR=0 timeout -k 10 200 python bench.py --eps 13 --test-mode --steps 400 --pmc off --no-cpu-baseline > $O/eps13_test_fast.json 2> $O/eps13_test_fast.err || exit 1
-timeout -k 10 300 python bench.py --eps 80 --lattice 8192 --steps 4 --warmup 1 --warmup-ms 0 --pmc off --no-cpu-baseline --kernel auto > $O/eps80_exact.json 2> $O/eps80_exact.err || exit 1
-timeout -k 10 300 python bench.py --eps 96 --lattice 8192 --steps 2 --warmup 1 --warmup-ms 0 --pmc off --no-cpu-baseline --kernel auto > $O/eps96_exact.json 2> $O/eps96_exact.err || exit 1
+timeout -k 10 300 python bench.py --eps 80 --lattice 8192 --steps 4 --warmup 1 --warmup-ms 0 --pmc off --no-cpu-baseline --kernel exact > $O/eps80_exact.json 2> $O/eps80_exact.err || exit 1
+timeout -k 10 300 python bench.py --eps 96 --lattice 8192 --steps 2 --warmup 1 --warmup-ms 0 --pmc off --no-cpu-baseline --kernel exact > $O/eps96_exact.json 2> $O/eps96_exact.err || exit 1
+for e in 65 80 96 97 128; do
+  timeout -k 10 200 python bench.py --eps $e --lattice 8192 --steps 20 --pmc off --no-cpu-baseline > $O/eps${e}_prefix.json 2> $O/eps${e}_prefix.err || exit 1
+done
 echo done > $O/done
