@@ -54,9 +54,11 @@ __device__ __forceinline__ double rt_wave_prefix(double x) {
 }
 
 // NV staged values per lane (window of 64 NV columns: 64 + 2 E rounded up
-// to even <= 64 NV),
-// R output rows per work item (seg_rows of the rect list)
-template <int NV, int R, bool TEST>
+// to even <= 64 NV), R output rows per work item (seg_rows of the rect
+// list).  SKIP: input rows whose horizon misses some of the R output rows
+// (the first and last R - 1 of the 2E + R) test each pair's row uniformly and
+// skip it, instead of adding the table's zero offsets
+template <int NV, int R, bool TEST, bool SKIP = false>
 __global__ __launch_bounds__(64) void k_prefix_rt(RectList L, StepConst C, const int2 *__restrict__ tab) {
   constexpr int NPF = 64 * NV + 2;  // doubles per prefix slot: [0] = P(-1) = 0, [1 + k] = P(k)
   __shared__ __attribute__((aligned(16))) double pf[2][NPF];
@@ -116,10 +118,21 @@ __global__ __launch_bounds__(64) void k_prefix_rt(RectList L, StepConst C, const
     // pairs: output j <- d = r - (y0 + j); table entry d + E + R
     const int2 *t = tab + (r - y0 + E + R);
     const double *cen = &pf[s][1 + EP + lane];  // the lane's P(c), c = EP + lane
+    const int jlo = r - y0 - E, jhi = r - y0 + E;  // outputs within this row's horizon
+    if (!SKIP || (jlo <= 0 && jhi >= R - 1)) {
 #pragma unroll
-    for (int j = 0; j < R; ++j) {
-      const int2 o = t[-j];  // {L, -L - 1}, or {0, 0} past the horizon
-      acc[j] += cen[o.x] - cen[o.y];
+      for (int j = 0; j < R; ++j) {
+        const int2 o = t[-j];  // {L, -L - 1}, or {0, 0} past the horizon
+        acc[j] += cen[o.x] - cen[o.y];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < R; ++j) {
+        if (j >= jlo && j <= jhi) {
+          const int2 o = t[-j];
+          acc[j] += cen[o.x] - cen[o.y];
+        }
+      }
     }
     asm volatile("" ::: "memory");
 #pragma unroll
