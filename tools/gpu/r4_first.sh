@@ -28,5 +28,5 @@ for e in 65 80 96 97 128; do
   timeout -k 10 200 python bench.py --eps $e --lattice 8192 --steps 20 --pmc off --no-cpu-baseline > $O/eps${e}_prefix.json 2> $O/eps${e}_prefix.err || exit 1
 done
 timeout -k 10 300 build/wide_bench_wpg 8192 20 > $O/wide_wpg.jsonl 2> $O/wide_wpg.err || exit 1
-timeout -k 10 300 build/prefix_bench 8192 10 48 64 80 96 128 > $O/prefix_bench.jsonl 2> $O/prefix_bench.err || exit 1
+timeout -k 10 300 build/prefix_bench 8192 10 32 40 48 56 64 80 96 128 > $O/prefix_bench.jsonl 2> $O/prefix_bench.err || exit 1
 echo done > $O/done

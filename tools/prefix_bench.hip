@@ -59,11 +59,16 @@ int main(int argc, char **argv) {
       {"R16_skip", k_prefix_rt<4, 16, false, true>, 16},
       {"R48_skip", k_prefix_rt<4, 48, false, true>, 48},
       {"R64_skip", k_prefix_rt<4, 64, false, true>, 64},
+      {"R32_run", k_prefix_rt<4, 32, false, false, true>, 32},
+      {"R48_run", k_prefix_rt<4, 48, false, false, true>, 48},
+      {"R64_run", k_prefix_rt<4, 64, false, false, true>, 64},
   };
   std::vector<Variant> vs8 = {
       {"R32", k_prefix_rt<8, 32, false, false>, 32},
       {"R32_skip", k_prefix_rt<8, 32, false, true>, 32},
       {"R48_skip", k_prefix_rt<8, 48, false, true>, 48},
+      {"R32_run", k_prefix_rt<8, 32, false, false, true>, 32},
+      {"R48_run", k_prefix_rt<8, 48, false, false, true>, 48},
   };
   for (int E : eps) {
     const int H = E, XL = (E + 7) / 8 * 8;
