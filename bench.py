@@ -266,6 +266,21 @@ def spawn_ranks(n: int) -> int:
     return rc
 
 
+class stdout_to_stderr:
+    """RCCL prints its version banner on stdout when a communicator starts:
+    keep fd 1 for the one JSON line (the banner goes to stderr)."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+
+
 def strong_reference(args) -> dict:
     """T1 of the strong-scaling efficiency T1 / (N T_N): this bench on ONE GPU
     over the same total lattice, run as a child process before this rank
@@ -414,9 +429,10 @@ def main() -> int:
         dist.broadcast_object_list(obj, src=0)
         comm_id = obj[0]
 
-    s = N.Solver(nx, ny, eps, 1.0, dt, dh, test=args.test_mode, kernel=args.kernel, device=local,
-                 rank=rank, nranks=nranks, tiles=(px, py), comm_id=comm_id, seg_rows=args.seg_rows,
-                 influence=args.influence)
+    with stdout_to_stderr():
+        s = N.Solver(nx, ny, eps, 1.0, dt, dh, test=args.test_mode, kernel=args.kernel, device=local,
+                     rank=rank, nranks=nranks, tiles=(px, py), comm_id=comm_id, seg_rows=args.seg_rows,
+                     influence=args.influence)
     info = s.info()
     # every rank owns exactly one block of the px x py grid, and the RCCL
     # communicator itself (ncclCommCount / ncclCommUserRank, nlh_info) must

@@ -27,7 +27,12 @@ static int launch_nv(const RectList &rl, const StepConst &c, const void *table, 
 int launch_prefix_rt(const RectList &rl, const StepConst &c, const void *table, bool test, void *stream) {
   hipStream_t st = (hipStream_t)stream;
   if (rl.nwork <= 0) return 0;
+  // the staged window 64 + 2E (rounded up to even) <= 64 NV columns; the
+  // narrowest NV that holds it (every staged value is loaded, scanned and
+  // written to LDS: eps 97 ran at 12.8 G node/s with NV = 8 against 23.4 G
+  // at eps 96 with NV = 4, profiles/r04/first/)
   if (c.E <= 96) return test ? launch_nv<4, true>(rl, c, table, st) : launch_nv<4, false>(rl, c, table, st);
+  if (c.E <= 160) return test ? launch_nv<6, true>(rl, c, table, st) : launch_nv<6, false>(rl, c, table, st);
   if (c.E <= 224) return test ? launch_nv<8, true>(rl, c, table, st) : launch_nv<8, false>(rl, c, table, st);
   return -1;
 }

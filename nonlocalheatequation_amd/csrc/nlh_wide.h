@@ -225,7 +225,10 @@ __global__ __launch_bounds__(64, 1) void k_wide(RectList L, StepConst C) {
       dma_chunks<W / 2>(l0 + (int64_t)k * stride, llw + slot * W * 8, lane);
       dma_chunks<1>(C.syt + (sy_index(fetched) & ~1), lsy + slot * 16, lane);
     }
-    dma_chunks<NCH>(gnext, lring + slot * RWS * 8, lane);
+    // default-policy (temporal) DMA: the neighbouring strips stage this row's
+    // halo columns again through the same XCD's L2 (C4: 167-169 vs 164-166 G
+    // node/s with nt, profiles/r04/first/wide_wpg.jsonl)
+    dma_chunks<NCH, false, false>(gnext, lring + slot * RWS * 8, lane);
     if constexpr (AB) dma_chunks<NCH>(gnext + 1, lring + (slot * RWS + OB) * 8, lane);
     ++fetched;
     if (fetched < n_in) gnext += stride;

@@ -235,6 +235,24 @@ def test_halo_plan_covers_halo_exactly(kernel, test, width):
             assert np.array_equal(got, need)
 
 
+@pytest.mark.parametrize("eps", [40, 64, 80, 150, 230])
+def test_halo_width_large_horizons(eps):
+    """Past the two-step horizons the fast kernels are single-step (k_wide to
+    64, k_prefix_rt to 224, k_exact beyond): halo = eps, in every mode."""
+    nx, ny, tiles, world = 600, 480, (3, 2), 2
+    for test in (False, True):
+        kw = dict(k=1.0, dt=eps ** 4 / (nx * nx * 8.0 * N.disk_count(eps)), dh=1.0 / nx, test=test, kernel="auto")
+        b = N.block_plan(nx, ny, eps, tiles, None, world, True, **kw)
+        pcs = N.halo_plan(nx, ny, eps, tiles, None, 0, world, True, **kw)
+        assert len(pcs) > 0
+        for src, dst, gx0, gy0, pw, ph, sb, db in pcs:
+            x0, y0, w, h = b[db][2:]
+            # every piece lies within eps of its destination block
+            assert x0 - eps <= gx0 and gx0 + pw <= x0 + w + eps and y0 - eps <= gy0 and gy0 + ph <= y0 + h + eps
+        assert max(max(x0 - p[2], p[2] + p[4] - (x0 + w), y0 - p[3], p[3] + p[5] - (y0 + h))
+                   for p in pcs for (x0, y0, w, h) in [b[p[7]][2:]]) == eps
+
+
 def test_default_owner_is_locidx():
     # locidx(): (i * nl) / (npx * npy)   src/2d_nonlocal_distributed.cpp:105-110
     o = N.resolve_owner(5, 5, 8)

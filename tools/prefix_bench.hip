@@ -53,15 +53,15 @@ int main(int argc, char **argv) {
   std::vector<int> eps;
   for (int i = 3; i < argc; ++i) eps.push_back(std::atoi(argv[i]));
   if (eps.empty()) eps = {48, 64, 80, 96};
+  // round 4 (profiles/r04/first/prefix_bench.jsonl): R = 32 without SKIP /
+  // RUN was the fastest everywhere (the uniform branches serialise the LDS
+  // reads; R 48 / 64 cost occupancy)
   std::vector<Variant> vs4 = {
-      {"R32", k_prefix_rt<4, 32, false, false>, 32},
-      {"R32_skip", k_prefix_rt<4, 32, false, true>, 32},
-      {"R16_skip", k_prefix_rt<4, 16, false, true>, 16},
-      {"R48_skip", k_prefix_rt<4, 48, false, true>, 48},
-      {"R64_skip", k_prefix_rt<4, 64, false, true>, 64},
-      {"R32_run", k_prefix_rt<4, 32, false, false, true>, 32},
-      {"R48_run", k_prefix_rt<4, 48, false, false, true>, 48},
-      {"R64_run", k_prefix_rt<4, 64, false, false, true>, 64},
+      {"R32", k_prefix_rt<4, 32, false>, 32},
+  };
+
+  std::vector<Variant> vs6 = {
+      {"NV6_R32", k_prefix_rt<6, 32, false>, 32},
   };
   std::vector<Variant> vs8 = {
       {"R32", k_prefix_rt<8, 32, false, false>, 32},
@@ -103,7 +103,7 @@ int main(int argc, char **argv) {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    const auto &vs = E <= 96 ? vs4 : vs8;
+    const auto &vs = E <= 96 ? vs4 : E <= 160 ? vs6 : vs8;
     for (size_t vi = 0; vi < vs.size(); ++vi) {
       const Variant &v = vs[vi];
       const std::vector<int32_t> tab = table(E, v.rows);

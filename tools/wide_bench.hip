@@ -33,6 +33,7 @@ struct Variant {
   KFn fn;
   int strip;      // output columns per strip
   int wg_per_cu;  // resident workgroups per CU
+  int threads = 64;  // 64 x waves per workgroup
 };
 
 #ifndef WB_E
@@ -79,19 +80,23 @@ int main(int argc, char **argv) {
   // variants: prefix-sum rows (production, PA = 0) and prefix rows built PA
   // rows ahead (k_wide PA), at DMA depths 6 and 8
 #if WB_E <= 32
-  // production (ILS + nt stores + row pairs) and row-pair variants of DMA
-  // depth D, prefix-ahead distance PA and chunk rows CH
+  // production (WPG 1: one wave per 64-column strip, nt DMA) vs shared staged
+  // rows (WPG waves per workgroup over one 64 WPG + 2 EP row) and the DMA's
+  // cache policy (DNT)
+#define KW(WPG, DNT) k_wide<E, 8, false, 6, 0, 1, false, 16, true, true, 2, true, true, true, true, WPG, DNT>
   std::vector<Variant> vs = {
-      {"rp_C8_D6_PA2", k_wide<E, 8, false, 6, 0, 1, false, 16, true, true, 2, true, true, true, true>, 64, 8},
-      {"rp_C8_D8_PA2", k_wide<E, 8, false, 8, 0, 1, false, 16, true, true, 2, true, true, true, true>, 64, 8},
-      {"rp_C8_D6_PA3", k_wide<E, 8, false, 6, 0, 1, false, 16, true, true, 3, true, true, true, true>, 64, 8},
-      {"rp_C6_D6_PA2", k_wide<E, 6, false, 6, 0, 1, false, 16, true, true, 2, true, true, true, true>, 64, 8},
-      {"rp_C4_D6_PA2", k_wide<E, 4, false, 6, 0, 1, false, 16, true, true, 2, true, true, true, true>, 64, 8},
-      {"one_row_C8_D6_PA2", k_wide<E, 8, false, 6, 0, 1, false, 16, true, true, 2, true, true, true, false>, 64, 8},
-      {"rp_C8_D6_PA2_b", k_wide<E, 8, false, 6, 0, 1, false, 16, true, true, 2, true, true, true, true>, 64, 8},
-      {"rp_C8_D8_PA2_b", k_wide<E, 8, false, 8, 0, 1, false, 16, true, true, 2, true, true, true, true>, 64, 8},
-      {"rp_C8_D6_PA3_b", k_wide<E, 8, false, 6, 0, 1, false, 16, true, true, 3, true, true, true, true>, 64, 8},
-      {"rp_C6_D6_PA2_b", k_wide<E, 6, false, 6, 0, 1, false, 16, true, true, 2, true, true, true, true>, 64, 8},
+      {"prod_wpg1_nt", KW(1, true), 64, 8, 64},
+      {"wpg1_dflt", KW(1, false), 64, 8, 64},
+      {"wpg2_nt", KW(2, true), 128, 4, 128},
+      {"wpg2_dflt", KW(2, false), 128, 4, 128},
+      {"wpg4_nt", KW(4, true), 256, 2, 256},
+      {"wpg4_dflt", KW(4, false), 256, 2, 256},
+      {"prod_wpg1_nt_b", KW(1, true), 64, 8, 64},
+      {"wpg1_dflt_b", KW(1, false), 64, 8, 64},
+      {"wpg2_nt_b", KW(2, true), 128, 4, 128},
+      {"wpg2_dflt_b", KW(2, false), 128, 4, 128},
+      {"wpg4_nt_b", KW(4, true), 256, 2, 256},
+      {"wpg4_dflt_b", KW(4, false), 256, 2, 256},
   };
 #else
   // nested windows, 8-row chunks (the production form past eps 35), one row
@@ -130,7 +135,7 @@ int main(int argc, char **argv) {
       for (int j = 0; j < k; ++j) {
         L.r[0].u = origin(buf[cur]);
         L.r[0].un = origin(buf[1 - cur]);
-        hipLaunchKernelGGL(v.fn, dim3(L.nwork), dim3(64), 0, 0, L, C);
+        hipLaunchKernelGGL(v.fn, dim3(L.nwork), dim3(v.threads), 0, 0, L, C);
         cur = 1 - cur;
       }
     };
