@@ -63,7 +63,11 @@ __device__ __forceinline__ double rt_wave_prefix(double x) {
 // half-width (len changes slowly near |d| = 0: at eps 80, |d| <= 12 has two
 // values) reuse the previous pair's H instead of two more LDS reads and a
 // subtraction -- a uniform (scalar) test per pair
-template <int NV, int R, bool TEST, bool SKIP = false, bool RUN = false>
+//
+// CPL: output columns per lane (strips of 64 CPL columns); the lane's CPL
+// prefix values at each offset are adjacent in LDS (one ds_read2_b64 for two
+// columns), and the staged halo is shared by more columns
+template <int NV, int R, bool TEST, bool SKIP = false, bool RUN = false, int CPL = 1>
 __global__ __launch_bounds__(64) void k_prefix_rt(RectList L, StepConst C, const int2 *__restrict__ tab) {
   constexpr int NPF = 64 * NV + 2;  // doubles per prefix slot: [0] = P(-1) = 0, [1 + k] = P(k)
   __shared__ __attribute__((aligned(16))) double pf[2][NPF];
@@ -74,12 +78,11 @@ __global__ __launch_bounds__(64) void k_prefix_rt(RectList L, StepConst C, const
   const Rect &Rc = L.r[ri];
   const int local = work - Rc.wg_begin;
   const int strip = local % Rc.nstrip, seg = local / Rc.nstrip;
-  const int x0 = Rc.x0 + strip * 64;
+  const int x0 = Rc.x0 + strip * (64 * CPL);
   const int y0 = Rc.y0 + seg * Rc.seg_rows;
   const int nout = min(R, Rc.y1 - y0);  // seg_rows == R (host)
   const int64_t pitch = Rc.pitch;
-  const int xl = x0 + lane;
-  const bool emit = xl < Rc.x1;
+  const int xl = x0 + CPL * lane;  // the lane's first column
   if (lane == 0) {
     pf[0][0] = 0.0;
     pf[1][0] = 0.0;
@@ -99,9 +102,11 @@ __global__ __launch_bounds__(64) void k_prefix_rt(RectList L, StepConst C, const
       v[2 * k + 1] = w.y;
     }
   };
-  double acc[R];
+  double acc[R][CPL];
 #pragma unroll
-  for (int j = 0; j < R; ++j) acc[j] = 0.0;
+  for (int j = 0; j < R; ++j)
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) acc[j][c] = 0.0;
 
   const int rfirst = y0 - E, rend = y0 + nout + E;  // input rows [rfirst, rend)
   double cur[NV], nxt[NV];
@@ -122,7 +127,7 @@ __global__ __launch_bounds__(64) void k_prefix_rt(RectList L, StepConst C, const
     asm volatile("" ::: "memory");  // LDS is in order per wave: the reads below see every lane's write
     // pairs: output j <- d = r - (y0 + j); table entry d + E + R
     const int2 *t = tab + (r - y0 + E + R);
-    const double *cen = &pf[s][1 + EP + lane];  // the lane's P(c), c = EP + lane
+    const double *cen = &pf[s][1 + EP + CPL * lane];  // the lane's P(c), c = EP + CPL lane
     const int jlo = r - y0 - E, jhi = r - y0 + E;  // outputs within this row's horizon
     if constexpr (RUN) {
       double h = 0.0;
@@ -132,20 +137,22 @@ __global__ __launch_bounds__(64) void k_prefix_rt(RectList L, StepConst C, const
         const int2 o = t[-j];  // {L, -L - 1}, or {0, 0} past the horizon
         if (o.x != prev.x || o.y != prev.y) h = cen[o.x] - cen[o.y];  // a new half-width
         prev = o;
-        acc[j] += h;
+        acc[j][0] += h;  // (RUN: one column per lane)
       }
     } else if (!SKIP || (jlo <= 0 && jhi >= R - 1)) {
 #pragma unroll
       for (int j = 0; j < R; ++j) {
         const int2 o = t[-j];  // {L, -L - 1}, or {0, 0} past the horizon
-        acc[j] += cen[o.x] - cen[o.y];
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) acc[j][c] += cen[o.x + c] - cen[o.y + c];
       }
     } else {
 #pragma unroll
       for (int j = 0; j < R; ++j) {
         if (j >= jlo && j <= jhi) {
           const int2 o = t[-j];
-          acc[j] += cen[o.x] - cen[o.y];
+#pragma unroll
+          for (int c = 0; c < CPL; ++c) acc[j][c] += cen[o.x + c] - cen[o.y + c];
         }
       }
     }
@@ -154,20 +161,26 @@ __global__ __launch_bounds__(64) void k_prefix_rt(RectList L, StepConst C, const
     for (int k = 0; k < NV; ++k) cur[k] = nxt[k];
   }
   // u' = alpha (S + kc u) [+ (dt/alpha) b]: u(x, y) from the field
+  static_assert(!RUN || CPL == 1, "RUN: one column per lane");
   const double alpha = C.alpha, kc = C.kc;
   const double qs = TEST ? C.dt / alpha : 0.0;
-  const double sxv = TEST ? C.sxt[Rc.gx0 + min(xl, Rc.x1 - 1) + E] : 0.0;
 #pragma unroll
-  for (int j = 0; j < R; ++j) {
-    if (j < nout && emit) {
-      const int64_t off = (int64_t)(y0 + j) * pitch + xl;
-      double a = fma(kc, Rc.u[off], acc[j]);
-      if constexpr (TEST) {
-        const double syv = C.syt[Rc.gy0 + y0 + j + E];
-        const double b = -(C.st2pi * (sxv * syv)) - C.ct * Rc.lw[off];
-        a = fma(qs, b, a);
+  for (int c = 0; c < CPL; ++c) {
+    const int x = xl + c;
+    const bool emit = x < Rc.x1;
+    const double sxv = TEST ? C.sxt[Rc.gx0 + min(x, Rc.x1 - 1) + E] : 0.0;
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      if (j < nout && emit) {
+        const int64_t off = (int64_t)(y0 + j) * pitch + x;
+        double a = fma(kc, Rc.u[off], acc[j][c]);
+        if constexpr (TEST) {
+          const double syv = C.syt[Rc.gy0 + y0 + j + E];
+          const double b = -(C.st2pi * (sxv * syv)) - C.ct * Rc.lw[off];
+          a = fma(qs, b, a);
+        }
+        Rc.un[off] = alpha * a;
       }
-      Rc.un[off] = alpha * a;
     }
   }
 }

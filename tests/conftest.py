@@ -65,29 +65,39 @@ def _record_dir() -> str:
 def check_l2(l2, l2_ref, u, u_ref, what: str = "") -> float:
     """The test-mode L2 criterion, recorded before it is asserted.
 
-    |l2 - l2_ref| <= 1e-10 * max(l2_ref, floor), floor = n * (1e-12 * max|u_ref|)^2:
-    1e-10 relative, except where the reference's own error_l2 sits below the
-    L2 a field differing by the per-node tolerance everywhere would have (the
-    rounding floor), where the bound is 1e-10 of that floor.  The observed
-    relative difference, the exact Cauchy-Schwarz bound the measured per-node
-    differences imply and the floor go to gpurun_out/parity_l2.jsonl.
-    Returns the relative difference."""
+    * 1e-10 relative, where the reference's own error per node is at least
+      1e-6 of the field scale (sqrt(l2_ref / n) >= 1e-6 max|u_ref|): every row of
+      the reference's batch files and the parity runs;
+    * where it is smaller the reference's L2 sits at the rounding floor of the
+      field -- per-node differences of a few ulp, far inside the 1e-12 per-node
+      tolerance, move it by more than 1e-10 relative (C4's 100 steps: 3.6e-10
+      per node, 6.5e-6 relative from 1.2e-15 rms differences) -- and the bound
+      is 1e-10 absolute;
+    * always: the L2 difference is the one the measured per-node differences
+      d imply, |l2 - l2_ref| <= 2 sqrt(l2_ref sum d^2) + sum d^2 (Cauchy-Schwarz)
+      up to the reductions' own rounding -- the norm kernel adds nothing.
+    The observed relative difference, that bound and the regime go to
+    gpurun_out/parity_l2.jsonl.  Returns the relative difference."""
     import json
 
     import numpy as np
     n = u_ref.size
     scale = float(np.max(np.abs(u_ref)))
-    floor = n * (1e-12 * scale) ** 2
     dd = float(np.sum((np.asarray(u, dtype=np.float64) - u_ref) ** 2))
-    cs = 2.0 * np.sqrt(l2_ref * dd) + dd  # |sum (e+d)^2 - sum e^2| <= 2 |e| |d| + |d|^2
-    rel = abs(l2 - l2_ref) / l2_ref if l2_ref > 0 else abs(l2 - l2_ref)
+    cs = 2.0 * np.sqrt(l2_ref * dd) + dd
+    diff = abs(l2 - l2_ref)
+    rel = diff / l2_ref if l2_ref > 0 else diff
+    relative = np.sqrt(l2_ref / n) >= 1e-6 * scale
     rec = {"test": os.environ.get("PYTEST_CURRENT_TEST", "").split(" ")[0], "what": what, "n": n,
-           "l2": l2, "l2_ref": l2_ref, "rel_diff": rel, "abs_diff": abs(l2 - l2_ref),
-           "cauchy_schwarz_bound": cs, "floor": floor, "max_node_diff": float(np.max(np.abs(u - u_ref)))}
+           "l2": l2, "l2_ref": l2_ref, "rel_diff": rel, "abs_diff": diff, "cauchy_schwarz_bound": cs,
+           "error_per_node_rms": float(np.sqrt(l2_ref / n)), "field_scale": scale,
+           "criterion": "1e-10 relative" if relative else "1e-10 absolute (rounding floor)",
+           "max_node_diff": float(np.max(np.abs(u - u_ref)))}
     try:
         with open(os.path.join(_record_dir(), "parity_l2.jsonl"), "a") as f:
             f.write(json.dumps(rec) + "\n")
     except OSError:
         pass
-    assert abs(l2 - l2_ref) <= 1e-10 * max(l2_ref, floor), rec
+    assert diff <= (1e-10 * l2_ref if relative else 1e-10), rec
+    assert diff <= cs * (1 + 1e-9) + 1e-13 * l2_ref + 1e-300, rec
     return rel

@@ -125,8 +125,8 @@ def test_virtual_busy_measured_per_rank(monkeypatch):
     group sized for the whole GPU as on the rank's own GPU, with the measured
     empty-launch overhead subtracted.  On an uneven map (1, 5, 4, 6 tiles of
     8192^2) busy time per tile agrees across ranks within 1.6x, so the busy
-    times follow the work; rebalancing from them evens the map to +-1 tile
-    and the spread of busy times shrinks; the field after the moves matches
+    times follow the work; rebalancing from them evens the measured busy
+    times (spread <= 1.5x); the field after the moves matches
     the same run on one block (fast kernel: 1e-12 of field scale)."""
     monkeypatch.setenv("NLH_VIRTUAL_RANKS", "4")
     T = 4
@@ -157,15 +157,15 @@ def test_virtual_busy_measured_per_rank(monkeypatch):
             m, cur, busy = s.rebalance()
             if m == 0:
                 break
-        cnt = np.bincount(cur, minlength=4)
-        assert cnt.max() - cnt.min() <= 1, cnt
         s.kernel_timing(2)
         s.run(20)
         s.synchronize()
         _, _, busy1 = s.rebalance(apply=False)
+        # the policy evens measured TIME, not tile counts: blocks of different
+        # shapes run at different rates (r04: 3 / 5 / 4 / 4 tiles balanced)
         spread0 = busy0.max() / busy0.min()
         spread1 = busy1.max() / busy1.min()
-        assert spread1 < 0.5 * spread0, (busy0, busy1, cur)
+        assert spread1 <= 1.5 and spread1 < 0.5 * spread0, (busy0, busy1, cur)
         s.run(6)
         s.synchronize()
         u = s.field()
@@ -290,9 +290,12 @@ def test_driver_nbalance_virtual_ranks(oracle, tmp_path):
 
 def test_driver_balances_large_tiles(tmp_path):
     """The same map with 2048^2 tiles (10240^2 lattice): busy time is kernel
-    work, so after the --nbalance rounds the tiles are spread to +-1 and the
-    reference's verdict (:682-685: busy-rate spread within 1500) reads "Load
-    balanced correctly"; the run still passes the batch contract l2/N <= 1e-6."""
+    work, so after the --nbalance rounds the reference's verdict (:682-685:
+    every busy rate within 1500 of the mean) reads "Load balanced correctly"
+    -- the map evens measured time, so tile counts may differ by more than
+    one (r04: 6 / 5 / 7 / 7 tiles at rates 2025 / 1823 / 2410 / 2148) -- the
+    rates are within [0, 10000] and sum to at most 10000 (the owners share
+    one GPU), and the run still passes the batch contract l2/N <= 1e-6."""
     f, npx, npy, own, R = _scaled_map(tmp_path, "load_balance_25s_4n.txt", 2048)
     env = dict(os.environ, NLH_VIRTUAL_RANKS=str(R))
     n = 2048 * npx
@@ -309,7 +312,7 @@ def test_driver_balances_large_tiles(tmp_path):
     j = lines.index("Visualizing Load Balance across nodes")
     grid = [list(map(int, lines[j + 1 + r].split())) for r in range(npx)]
     cnt = np.bincount(np.array(grid).ravel(), minlength=R)
-    assert cnt.max() - cnt.min() <= 1, (cnt, rates)
+    assert cnt.min() >= 1 and all(0 <= r <= 10000 for r in rates) and sum(rates) <= 10000 * 1.001, (rates, cnt)
     assert lines[j + 1 + npx] == "Load balanced correctly", (rates, cnt)
     m = re.search(r"^l2: (\S+) linfinity: (\S+)$", out.stdout, re.M)
     assert m and float(m.group(1)) / (n * n) <= 1e-6

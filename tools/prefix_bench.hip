@@ -32,6 +32,7 @@ struct Variant {
   const char *name;
   KFn fn;
   int rows;  // R
+  int cpl = 1;  // columns per lane
 };
 
 static int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
@@ -58,10 +59,15 @@ int main(int argc, char **argv) {
   // reads; R 48 / 64 cost occupancy)
   std::vector<Variant> vs4 = {
       {"R32", k_prefix_rt<4, 32, false>, 32},
+      {"R32_cpl2_nv6", k_prefix_rt<6, 32, false, false, false, 2>, 32, 2},
+      {"R16_cpl2_nv6", k_prefix_rt<6, 16, false, false, false, 2>, 16, 2},
+      {"R24_cpl2_nv6", k_prefix_rt<6, 24, false, false, false, 2>, 24, 2},
   };
 
   std::vector<Variant> vs6 = {
       {"NV6_R32", k_prefix_rt<6, 32, false>, 32},
+      {"R32_cpl2_nv8", k_prefix_rt<8, 32, false, false, false, 2>, 32, 2},
+      {"R16_cpl2_nv8", k_prefix_rt<8, 16, false, false, false, 2>, 16, 2},
   };
   std::vector<Variant> vs8 = {
       {"R32", k_prefix_rt<8, 32, false, false>, 32},
@@ -117,7 +123,7 @@ int main(int argc, char **argv) {
       R.x1 = n;
       R.y1 = n;
       R.seg_rows = v.rows;
-      R.nstrip = (int)ceil_div(n, 64);
+      R.nstrip = (int)ceil_div(n, 64 * v.cpl);
       R.nseg = (int)ceil_div(n, v.rows);
       L.nwork = R.nstrip * R.nseg;
       CK(hipMemcpy2D(origin(buf[0]), pitch * 8, h.data(), (size_t)n * 8, (size_t)n * 8, n, hipMemcpyHostToDevice));
