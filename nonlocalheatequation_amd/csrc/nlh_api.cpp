@@ -386,7 +386,10 @@ int build_rectlists(nlh_solver *s, int kind) {
   // k_weighted tiles like k_exact (64-column strips, fixed segments)
   const bool fast = s->kernel == NLH_KERNEL_FAST && !s->weighted;
   const bool pair = kind == 1;
-  const int sw = pair ? nlh::pair_strip_width(E) : fast ? nlh::fast_strip_width(E, s->fast_r) : 64;
+  const int sw = pair        ? nlh::pair_strip_width(E)
+                 : !fast     ? 64
+                 : s->prefix ? nlh::prefix_rt_strip_width(E)
+                             : nlh::fast_strip_width(E, s->fast_r);
   // gather local rects (bands are s->halo wide: what the halo exchange refreshes)
   struct Item { int blk; LRect r; };
   std::vector<Item> all, inter, bnd;

@@ -7,6 +7,10 @@ bool prefix_rt_supported(int E) { return E >= 65 && E <= 224; }
 
 int prefix_rt_table_size(int E) { return 2 * (E + kPrefixRows) + 1; }
 
+// columns per lane of the launched instances (launch_prefix_rt)
+static int prefix_rt_cpl(int) { return 1; }
+int prefix_rt_strip_width(int E) { return 64 * prefix_rt_cpl(E); }
+
 void prefix_rt_table(int E, const int32_t *lens, int32_t *out) {
   for (int i = 0; i < prefix_rt_table_size(E); ++i) {
     const int d = i - E - kPrefixRows;

@@ -13,6 +13,8 @@ bool prefix_rt_supported(int E);
 // host table of 2 (E + R) + 1 int2 entries, index d + E + R: {L, -L - 1}
 // with L = len(|d|) for |d| <= E, {0, 0} beyond
 int prefix_rt_table_size(int E);
+// output columns per work item (64 x the kernel's columns per lane)
+int prefix_rt_strip_width(int E);
 void prefix_rt_table(int E, const int32_t *lens, int32_t *out);
 int launch_prefix_rt(const RectList &rl, const StepConst &c, const void *table, bool test, void *stream);
 
