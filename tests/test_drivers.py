@@ -156,3 +156,19 @@ def test_serial_linear_influence_flag(oracle):
                        capture_output=True, text=True, timeout=60)
     assert p.returncode != 0
 
+
+
+@pytest.mark.parametrize("eps", [70, 100])
+def test_serial_driver_large_horizon(oracle, eps):
+    """--eps past the compile-time horizons (the reference accepts any,
+    src/2d_nonlocal_serial.cpp:403): the serial driver's AUTO route runs
+    k_prefix_rt; its printed l2 / linfinity match the oracle's (6 digits)."""
+    nx, nt = 160, 3
+    dh = 1.0 / nx
+    dt = 0.05 * eps ** 4 * dh * dh / (8 * oracle.disk_count(eps))
+    out = run("2d_nonlocal_serial", ["--test", "--cmp", "false", "--nx", str(nx), "--ny", str(nx), "--nt", str(nt),
+                                     "--eps", str(eps), "--dt", repr(dt), "--dh", repr(dh), "--nlog", "1000"])
+    p = oracle.params(nx, nx, eps, 1.0, dt, dh, 1)
+    l2, li = oracle.errors(p, nt, oracle.run(p, nt))
+    m = re.search(r"^l2: (\S+) linfinity: (\S+)$", out, re.M)
+    assert m and float(m.group(1)) == pytest.approx(l2, rel=1e-5) and float(m.group(2)) == pytest.approx(li, rel=1e-5)
