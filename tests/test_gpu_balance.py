@@ -178,6 +178,43 @@ def test_virtual_busy_measured_per_rank(monkeypatch):
     assert np.max(np.abs(u - ref)) <= 1e-12 * np.max(np.abs(ref))
 
 
+def test_repartition_large_messages(monkeypatch):
+    """Tile moves of more than 1 GiB per rank pair: on 8192^2 tiles the
+    1 / 5 / 4 / 6 map -> an even one sends three tiles (1.5 GiB) from rank 1 to
+    rank 0 in one message, and the root gather of rank 3's six tiles is 3 GiB.
+    The field after the move, stepped on, and the gathered field match one
+    block (fast kernel: 1e-12 of field scale).  Before the messages were
+    chunked the second and third tiles of the 1.5 GiB message never arrived
+    (profiles/r04/fourth/diag_8192.log)."""
+    monkeypatch.setenv("NLH_VIRTUAL_RANKS", "4")
+    T = 4
+    own = np.array([0, 1, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 3, 3], np.int32)
+    even = np.array([0, 0, 1, 1, 0, 0, 1, 1, 2, 2, 3, 3, 2, 2, 3, 3], np.int32)
+    nx = ny = T * 8192
+    eps = 8
+    dh = 1.0 / nx
+    dt = eps ** 4 * dh * dh / (8 * N.disk_count(eps))
+    with N.Solver(nx, ny, eps, 1.0, dt, dh, kernel="fast", tiles=(T, T), owner=own) as s:
+        s.test_init()
+        s.run(4)
+        g = s.gather(0)
+        s.repartition(even)
+        s.run(6)
+        s.synchronize()
+        u = s.field()
+    monkeypatch.delenv("NLH_VIRTUAL_RANKS")
+    with N.Solver(nx, ny, eps, 1.0, dt, dh, kernel="fast") as r:
+        r.test_init()
+        r.run(4)
+        ref4 = r.field()
+        r.run(6)
+        ref = r.field()
+    scale = np.max(np.abs(ref))
+    assert np.max(np.abs(g - ref4)) <= 1e-12 * scale
+    del g, ref4
+    assert np.max(np.abs(u - ref)) <= 1e-12 * scale
+
+
 def test_busy_time_within_wall_time():
     """Busy timing serialises a pass's kernels on one stream, so a rank's busy
     time never exceeds the wall time of the window (the reference's busy rate
