@@ -2,7 +2,8 @@
 # Round 4 evidence at the library build the round ends on: per workload the
 # bench line, the rocprofv3 --kernel-trace --stats summary of the same
 # command, PMC passes over tools/prof_step.py and the PMC record
-# (tools/bench_evidence.sh), plus the GPU suite and smoke at that build.
+# (tools/bench_evidence.sh), and the driver's 20-step C2 line.  The GPU suite
+# and smoke at the same build run in their own call (tools/gpu/r4_fifth.sh).
 #   bash tools/gpu/r4_evidence.sh COMMIT   -> gpurun_out/r4e/<workload>/
 # committed as profiles/r04/evidence/; the PMC records also as profiles/pmc/.
 set -o pipefail
