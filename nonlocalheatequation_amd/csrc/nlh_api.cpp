@@ -1136,18 +1136,22 @@ int create_impl(const nlh_params *pin, nlh_solver *s, ncclComm_t reuse_comm = nu
     b.T = b.r.y0 > 0 || s->force_bands;
     b.B = b.r.y0 + b.r.h < p.ny || s->force_bands;
     const size_t bytes = (size_t)(b.pitch * b.rows) * sizeof(double);
+    // zeroed on s_main (a non-blocking stream: a null-stream hipMemset is not
+    // ordered before work on it), and waited for below, before anything --
+    // test_init, set_field, a repartition's tile copies -- writes the blocks
     for (int k = 0; k < 2; ++k) {
       HIP_TRY(hipMalloc(&b.base[k], bytes));
-      HIP_TRY(hipMemset(b.base[k], 0, bytes));
+      HIP_TRY(hipMemsetAsync(b.base[k], 0, bytes, s->s_main));
       s->device_bytes += (int64_t)bytes;
     }
     if (kern == NLH_KERNEL_FAST && p.test) {
       HIP_TRY(hipMalloc(&b.lw_base, bytes));
-      HIP_TRY(hipMemset(b.lw_base, 0, bytes));
+      HIP_TRY(hipMemsetAsync(b.lw_base, 0, bytes, s->s_main));
       s->device_bytes += (int64_t)bytes;
     }
     s->blocks.push_back(b);
   }
+  HIP_TRY(hipStreamSynchronize(s->s_main));
 
   s->exchange_planned = !s->plan.pieces.empty() || s->force_bands;
   int rc = build_rectlists(s, 0);
@@ -1202,22 +1206,6 @@ int create_impl(const nlh_params *pin, nlh_solver *s, ncclComm_t reuse_comm = nu
     if (rc) return rc;
   }
   return NLH_OK;
-}
-
-// A point-to-point message of cnt doubles, posted (inside the caller's group)
-// as chunks of at most kP2PChunk doubles (256 MiB) in order.  A single
-// 1.5 GiB send/recv to self -- three 8192^2 tiles in one repartition message --
-// delivered only its first 512 MiB (profiles/r04/fourth/diag_8192.log); 1 GiB
-// messages arrived whole.  Chunks match pairwise in order on both sides.
-constexpr size_t kP2PChunk = size_t(1) << 25;
-bool p2p(bool send, double *buf, size_t cnt, int peer, ncclComm_t comm, hipStream_t st) {
-  for (size_t o = 0; o < cnt; o += kP2PChunk) {
-    const size_t c = std::min(kP2PChunk, cnt - o);
-    if ((send ? ncclSend(buf + o, c, ncclDouble, peer, comm, st) : ncclRecv(buf + o, c, ncclDouble, peer, comm, st)) !=
-        ncclSuccess)
-      return false;
-  }
-  return true;
 }
 
 // the plan block holding global node (x, y): its rank and local block index
@@ -1384,14 +1372,16 @@ int repartition_impl(nlh_solver *s, const std::vector<int32_t> &own) {
         for (auto &kv : sends) {  // A -> B: A's staged tiles into B's staging buffer, over RCCL to self
           const size_t cnt = kv.second.size() * tb;
           ok = ok && recvs.count(kv.first) && recvs[kv.first].size() == kv.second.size();
-          for (size_t o = 0; ok && o < cnt; o += kP2PChunk) {
-            const size_t c = std::min(kP2PChunk, cnt - o);
-            ok = p2p(true, sbuf[kv.first] + o, c, 0, n->comm, st) && p2p(false, rbuf[kv.first] + o, c, 0, n->comm, st);
-          }
+          ok = ok && ncclSend(sbuf[kv.first], cnt, ncclDouble, 0, n->comm, st) == ncclSuccess;
+          ok = ok && ncclRecv(rbuf[kv.first], cnt, ncclDouble, 0, n->comm, st) == ncclSuccess;
         }
       } else {
-        for (auto &kv : sends) ok = ok && p2p(true, sbuf[kv.first], kv.second.size() * tb, kv.first.second, n->comm, st);
-        for (auto &kv : recvs) ok = ok && p2p(false, rbuf[kv.first], kv.second.size() * tb, kv.first.first, n->comm, st);
+        for (auto &kv : sends)
+          ok = ok && ncclSend(sbuf[kv.first], kv.second.size() * tb, ncclDouble, kv.first.second, n->comm, st) ==
+                         ncclSuccess;
+        for (auto &kv : recvs)
+          ok = ok && ncclRecv(rbuf[kv.first], kv.second.size() * tb, ncclDouble, kv.first.first, n->comm, st) ==
+                         ncclSuccess;
       }
       ok = (ncclGroupEnd() == ncclSuccess) && ok;
       if (!ok) status = fail(NLH_ERR_RCCL, "repartition send/recv");
@@ -1631,8 +1621,8 @@ int nlh_gather_field(nlh_solver *s, int32_t root, double *u) {
     if (status != NLH_OK) break;
     bool ok = ncclGroupStart() == ncclSuccess;
     const int to = s->vranks ? 0 : root, from = s->vranks ? 0 : r;
-    if (sender) ok = ok && p2p(true, sbuf, count[r], to, s->comm, s->s_comm);
-    if (at_root) ok = ok && p2p(false, rbuf, count[r], from, s->comm, s->s_comm);
+    if (sender) ok = ok && ncclSend(sbuf, count[r], ncclDouble, to, s->comm, s->s_comm) == ncclSuccess;
+    if (at_root) ok = ok && ncclRecv(rbuf, count[r], ncclDouble, from, s->comm, s->s_comm) == ncclSuccess;
     ok = (ncclGroupEnd() == ncclSuccess) && ok;
     if (!ok) {
       status = fail(NLH_ERR_RCCL, "gather send/recv");

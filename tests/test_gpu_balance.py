@@ -178,18 +178,22 @@ def test_virtual_busy_measured_per_rank(monkeypatch):
     assert np.max(np.abs(u - ref)) <= 1e-12 * np.max(np.abs(ref))
 
 
-def test_repartition_large_messages(monkeypatch):
-    """Tile moves of more than 1 GiB per rank pair: on 8192^2 tiles the
-    1 / 5 / 4 / 6 map -> an even one sends three tiles (1.5 GiB) from rank 1 to
-    rank 0 in one message, and the root gather of rank 3's six tiles is 3 GiB.
-    The field after the move, stepped on, and the gathered field match one
-    block (fast kernel: 1e-12 of field scale).  Before the messages were
-    chunked the second and third tiles of the 1.5 GiB message never arrived
-    (profiles/r04/fourth/diag_8192.log)."""
+@pytest.mark.parametrize("target", [
+    [0, 0, 1, 1, 0, 0, 1, 1, 2, 2, 3, 3, 2, 2, 3, 3],   # 3 tiles 1 -> 0, 2 -> 1, 3 -> 2
+    [0, 1, 1, 1, 0, 1, 2, 2, 2, 2, 3, 3, 0, 3, 3, 3],   # 1 -> 0 and 3 -> 0 into two new blocks
+])
+def test_repartition_large_messages(monkeypatch, target):
+    """Tile moves at 8192^2 tiles: the 1 / 5 / 4 / 6 map -> an even one sends
+    three tiles (1.5 GiB) from rank 1 to rank 0 in one message into a freshly
+    allocated 2 x 2-tile block, and the root gather of rank 3's six tiles is
+    3 GiB.  The field after the move, stepped on, and the gathered field match
+    one block (fast kernel: 1e-12 of field scale).  Before the new solver's
+    blocks were zeroed on its own stream (and waited for), the null-stream
+    memset could land after the moved tiles and zero them
+    (profiles/r04/fourth/diag_8192.log, profiles/r04/fifth/diag_8192.log)."""
     monkeypatch.setenv("NLH_VIRTUAL_RANKS", "4")
     T = 4
     own = np.array([0, 1, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 3, 3], np.int32)
-    even = np.array([0, 0, 1, 1, 0, 0, 1, 1, 2, 2, 3, 3, 2, 2, 3, 3], np.int32)
     nx = ny = T * 8192
     eps = 8
     dh = 1.0 / nx
@@ -198,7 +202,7 @@ def test_repartition_large_messages(monkeypatch):
         s.test_init()
         s.run(4)
         g = s.gather(0)
-        s.repartition(even)
+        s.repartition(np.array(target, np.int32))
         s.run(6)
         s.synchronize()
         u = s.field()

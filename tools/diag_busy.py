@@ -52,9 +52,12 @@ def virtual(prog):
     """prog: list of ("timing", mode) / ("run", n) / ("move", map) /
     ("rebalance", None)."""
     os.environ["NLH_VIRTUAL_RANKS"] = "4"
-    with N.Solver(nx, ny, eps, 1.0, dt, dh, kernel="fast", tiles=(T, T), owner=OWN) as s:
+    own = M7 if prog[0][0] == "start" else OWN
+    with N.Solver(nx, ny, eps, 1.0, dt, dh, kernel="fast", tiles=(T, T), owner=own) as s:
         s.test_init()
         for op, a in prog:
+            if op == "start":
+                continue
             if op == "timing":
                 s.kernel_timing(a)
             elif op == "run":
@@ -80,7 +83,15 @@ CASES = [
     ("timing 2, move after 4, +6", [("timing", 2), ("run", 4), ("move", EVEN), ("run", 6)]),
     ("run 4, timing 2, run 20, rebalance, run 6",
      [("run", 4), ("timing", 2), ("run", 20), ("rebalance", None), ("run", 6)]),
+    ("run 4, move to M7 (no steps after)", [("run", 4), ("move", None)]),
+    ("run 4, move to M7, run 6", [("run", 4), ("move", None), ("run", 6)]),
+    ("timing 2, run 4, move to M7, run 6", [("timing", 2), ("run", 4), ("move", None), ("run", 6)]),
+    ("run 24, move to M7, run 6", [("run", 24), ("move", None), ("run", 6)]),
+    ("M7 from the start, run 6", [("start", None), ("run", 6)]),
 ]
+# the map case 7's rebalance chose on 8192^2 tiles (profiles/r04/fifth)
+M7 = np.array([0, 1, 1, 1, 0, 1, 2, 2, 2, 2, 3, 3, 0, 3, 3, 3], np.int32)
+CASES = [(n, [(op, M7 if op == "move" and a is None else a) for op, a in p]) for n, p in CASES]
 only = sys.argv[2:] and set(int(a) for a in sys.argv[2:])
 for i, (name, prog) in enumerate(CASES):
     if only and i not in only:
