@@ -1208,6 +1208,24 @@ int create_impl(const nlh_params *pin, nlh_solver *s, ncclComm_t reuse_comm = nu
   return NLH_OK;
 }
 
+// A point-to-point message of cnt doubles, posted (inside the caller's group)
+// as in-order chunks of at most kP2PChunk doubles (256 MiB).  With RCCL
+// 2.27.7 on MI355X a single 1.5 GiB send/recv to self (three 8192^2 tiles of a
+// repartition) delivered only its first 512 MiB and a 3 GiB root gather
+// arrived corrupted, in every run; 0.5 and 1 GiB messages arrived whole
+// (profiles/r04/{fourth,fifth,sixth}: diag_8192.log, the large-move test).
+// The chunks match pairwise in order on both sides.
+constexpr size_t kP2PChunk = size_t(1) << 25;
+bool p2p(bool send, double *buf, size_t cnt, int peer, ncclComm_t comm, hipStream_t st) {
+  for (size_t o = 0; o < cnt; o += kP2PChunk) {
+    const size_t c = std::min(kP2PChunk, cnt - o);
+    if ((send ? ncclSend(buf + o, c, ncclDouble, peer, comm, st) : ncclRecv(buf + o, c, ncclDouble, peer, comm, st)) !=
+        ncclSuccess)
+      return false;
+  }
+  return true;
+}
+
 // the plan block holding global node (x, y): its rank and local block index
 void locate(const nlh_solver *s, int64_t x, int64_t y, int &rank, int &local) {
   rank = -1;
@@ -1372,16 +1390,14 @@ int repartition_impl(nlh_solver *s, const std::vector<int32_t> &own) {
         for (auto &kv : sends) {  // A -> B: A's staged tiles into B's staging buffer, over RCCL to self
           const size_t cnt = kv.second.size() * tb;
           ok = ok && recvs.count(kv.first) && recvs[kv.first].size() == kv.second.size();
-          ok = ok && ncclSend(sbuf[kv.first], cnt, ncclDouble, 0, n->comm, st) == ncclSuccess;
-          ok = ok && ncclRecv(rbuf[kv.first], cnt, ncclDouble, 0, n->comm, st) == ncclSuccess;
+          for (size_t o = 0; ok && o < cnt; o += kP2PChunk) {
+            const size_t c = std::min(kP2PChunk, cnt - o);
+            ok = p2p(true, sbuf[kv.first] + o, c, 0, n->comm, st) && p2p(false, rbuf[kv.first] + o, c, 0, n->comm, st);
+          }
         }
       } else {
-        for (auto &kv : sends)
-          ok = ok && ncclSend(sbuf[kv.first], kv.second.size() * tb, ncclDouble, kv.first.second, n->comm, st) ==
-                         ncclSuccess;
-        for (auto &kv : recvs)
-          ok = ok && ncclRecv(rbuf[kv.first], kv.second.size() * tb, ncclDouble, kv.first.first, n->comm, st) ==
-                         ncclSuccess;
+        for (auto &kv : sends) ok = ok && p2p(true, sbuf[kv.first], kv.second.size() * tb, kv.first.second, n->comm, st);
+        for (auto &kv : recvs) ok = ok && p2p(false, rbuf[kv.first], kv.second.size() * tb, kv.first.first, n->comm, st);
       }
       ok = (ncclGroupEnd() == ncclSuccess) && ok;
       if (!ok) status = fail(NLH_ERR_RCCL, "repartition send/recv");
@@ -1621,8 +1637,8 @@ int nlh_gather_field(nlh_solver *s, int32_t root, double *u) {
     if (status != NLH_OK) break;
     bool ok = ncclGroupStart() == ncclSuccess;
     const int to = s->vranks ? 0 : root, from = s->vranks ? 0 : r;
-    if (sender) ok = ok && ncclSend(sbuf, count[r], ncclDouble, to, s->comm, s->s_comm) == ncclSuccess;
-    if (at_root) ok = ok && ncclRecv(rbuf, count[r], ncclDouble, from, s->comm, s->s_comm) == ncclSuccess;
+    if (sender) ok = ok && p2p(true, sbuf, count[r], to, s->comm, s->s_comm);
+    if (at_root) ok = ok && p2p(false, rbuf, count[r], from, s->comm, s->s_comm);
     ok = (ncclGroupEnd() == ncclSuccess) && ok;
     if (!ok) {
       status = fail(NLH_ERR_RCCL, "gather send/recv");

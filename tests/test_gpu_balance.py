@@ -185,12 +185,15 @@ def test_virtual_busy_measured_per_rank(monkeypatch):
 def test_repartition_large_messages(monkeypatch, target):
     """Tile moves at 8192^2 tiles: the 1 / 5 / 4 / 6 map -> an even one sends
     three tiles (1.5 GiB) from rank 1 to rank 0 in one message into a freshly
-    allocated 2 x 2-tile block, and the root gather of rank 3's six tiles is
-    3 GiB.  The field after the move, stepped on, and the gathered field match
-    one block (fast kernel: 1e-12 of field scale).  Before the new solver's
-    blocks were zeroed on its own stream (and waited for), the null-stream
-    memset could land after the moved tiles and zero them
-    (profiles/r04/fourth/diag_8192.log, profiles/r04/fifth/diag_8192.log)."""
+    allocated 2 x 2-tile block; the other map moves two tiles into two new
+    blocks of rank 0; the root gather of rank 3's six tiles is 3 GiB.  The
+    gathered field, and the field after the move stepped on, match one block
+    (fast kernel: 1e-12 of field scale).  Two round-4 fixes are under test
+    (profiles/r04/{fourth,fifth,sixth}/diag_8192.log): messages go as
+    <= 256 MiB chunks (unchunked, the 1.5 GiB message delivered only its first
+    tile and the 3 GiB gather arrived corrupted), and a new solver zeroes its
+    blocks on its own stream and waits (a null-stream memset could land after
+    the moved tiles and zero them)."""
     monkeypatch.setenv("NLH_VIRTUAL_RANKS", "4")
     T = 4
     own = np.array([0, 1, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 3, 3], np.int32)
