@@ -63,6 +63,12 @@ def decomposition(n: int):
     return px, n // px
 
 
+def progress(msg: str) -> None:
+    """A progress line on stderr (stdout carries only the JSON line): a long
+    bench (live PMC passes, the CPU baseline) keeps writing while it runs."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def host_cpu_share() -> int:
     """Host threads this job may use: the CPU affinity mask, capped by the
     cgroup CPU quota and by OMP_NUM_THREADS when the launcher sets it (the GPU
@@ -96,16 +102,33 @@ def cpu_baseline(nthreads: int, nb: int = NB, eps: int = EPS, test: bool = False
     p = O.params(nb, nb, eps, 1.0, dt, dh, int(test))
     u = O.test_init(p)
     tiles = max(1, nb // 128)  # 128 x 128-node tiles
-    t1 = O.run_tiled(p, 1, tiles, tiles, u, nthreads)
-    if t1 > budget_s / 3:  # one step already fills the budget (C4's 8192^2 at eps 32): it is the sample
-        steps, t = 1, t1
+    th = -(-nb // tiles)
+    # probe: one tile row from the middle of the lattice -> the cost of a whole step
+    mid = (tiles // 2) * tiles
+    tp = O.time_tiles(p, 0, tiles, tiles, mid, tiles, u, nthreads)
+    if tp * tiles <= budget_s:
+        t1 = O.run_tiled(p, 1, tiles, tiles, u, nthreads)
+        if t1 > budget_s / 3:  # one step fills the budget: it is the sample
+            steps, t = 1, t1
+        else:
+            steps = int(max(1, min(200, budget_s / max(t1, 1e-3) - 1)))
+            t = O.run_tiled(p, steps, tiles, tiles, u, nthreads)
+        rate = nb * nb * steps / t / 1e9
+        what = (f"{steps} step(s) ({t:.1f} s{'' if steps == 1 and t == t1 else ', after 1 warm-up step'})")
     else:
-        steps = int(max(1, min(200, budget_s / max(t1, 1e-3) - 1)))
-        t = O.run_tiled(p, steps, tiles, tiles, u, nthreads)
-    rate = nb * nb * steps / t / 1e9
+        # a whole step would take ~tp * tiles s (C4's 8192^2 at eps 32: ~2 min):
+        # time the centre tile rows of one step of the same lattice, as many as
+        # fill the budget
+        rows = int(min(tiles, max(1, budget_s / tp)))
+        first = ((tiles - rows) // 2) * tiles
+        t = O.time_tiles(p, 0, tiles, tiles, first, rows * tiles, u, nthreads)
+        steps = 1
+        rate = rows * th * nb / t / 1e9
+        what = (f"the centre {rows} of its {tiles} tile rows of one step ({t:.1f} s; a whole step "
+                f"~{tp * tiles:.0f} s)")
     # single core: a square lattice of the same eps / mode sized from the
     # tiled per-thread rate, one step of the serial restatement
-    per_thread = nb * nb * steps / t / max(1, nthreads)
+    per_thread = rate * 1e9 / max(1, nthreads)
     side = int(min(nb, max(64, math.sqrt(serial_budget_s * per_thread)))) // 64 * 64
     ps = O.params(side, side, eps, 1.0, eps ** 4 / (8.0 * side * side * N.disk_count(eps)), 1.0 / side, int(test))
     us = O.test_init(ps)
@@ -117,8 +140,7 @@ def cpu_baseline(nthreads: int, nb: int = NB, eps: int = EPS, test: bool = False
                         f"oracle/nlh_oracle.c nlh_oracle_run on one thread (2d_nonlocal_serial restatement)"}
     return {"value": rate, "unit": "Gnode-updates/s", "cores": nthreads, "kind": "port",
             "host_cpus_visible": os.cpu_count(),
-            "sample": f"{nb}x{nb} lattice, eps={eps}, test={int(test)}, {steps} step(s) "
-                      f"({t:.1f} s{'' if steps == 1 and t == t1 else ', after 1 warm-up step'}), "
+            "sample": f"{nb}x{nb} lattice, eps={eps}, test={int(test)}, {what}, "
                       f"{tiles}x{tiles} tiles on {nthreads} threads (the job's host CPU share), "
                       f"oracle/nlh_oracle.c run_tiled (-O3 -ffp-contract=off)",
             "serial_1core": serial}
@@ -179,6 +201,7 @@ def live_pmc(args, wkey: str):
     vals, durs, seen = {}, {}, set()
     with tempfile.TemporaryDirectory(dir="/tmp") as td:
         for i, grp in enumerate(PMC_PASSES):
+            progress(f"live PMC pass {i + 1}/{len(PMC_PASSES)}: {grp}")
             out = os.path.join(td, f"p{i}")
             cmd = ["timeout", "-s", "KILL", "120", prof, "--pmc", *grp.split(), "--kernel-trace",
                    "--output-format", "csv", "-d", out, "-o", "run", "--",
@@ -293,6 +316,7 @@ def strong_reference(args) -> dict:
            "--kernel", args.kernel, "--influence", args.influence, "--pmc", "off", "--no-cpu-baseline"]
     if args.test_mode:
         cmd.append("--test-mode")
+    progress("strong scaling: the 1-GPU reference run of the same lattice")
     try:
         r = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=900)
     except (OSError, subprocess.SubprocessError) as e:
@@ -480,6 +504,8 @@ def main() -> int:
             dist.barrier()
 
     barrier()
+    if rank == 0:
+        progress(f"warm-up done ({warm} steps); timing {args.steps} steps")
     # HIP events on the stencil stream bracket the timed region (one pair);
     # the average launch duration below is their span / launches
     s.kernel_timing(True)
@@ -578,6 +604,7 @@ def main() -> int:
         if not args.no_cpu_baseline and nranks == 1 and args.influence == "constant":
             # bounded sample on the workload's own lattice (one step when that
             # fills the budget: C4) and a single-core serial leg
+            progress("CPU baseline (bounded sample, after the timed region)")
             cpu = cpu_baseline(host_cpu_share(), nb, eps, args.test_mode)
         result = {
             "metric": f"Gnode-updates/s (nodes*steps/s) eps={eps} fp64",

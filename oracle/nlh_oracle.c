@@ -150,18 +150,20 @@ typedef struct {
   const double *u;
   double *un;
   long tiles_x, tiles_y, tw, th;
+  long first, ntiles;  /* tiles first .. first+ntiles-1 of this step (all, or a timing sample) */
   long next_tile;
   pthread_mutex_t mu;
 } tile_job;
 
 static void *tile_worker(void *arg) {
   tile_job *j = (tile_job *)arg;
-  const long ntiles = j->tiles_x * j->tiles_y;
+  const long ntiles = j->ntiles;
   for (;;) {
     pthread_mutex_lock(&j->mu);
-    const long t = j->next_tile++;
+    const long k = j->next_tile++;
     pthread_mutex_unlock(&j->mu);
-    if (t >= ntiles) break;
+    if (k >= ntiles) break;
+    const long t = j->first + k;
     const long gx = t % j->tiles_x, gy = t / j->tiles_x;
     const long x0 = gx * j->tw, y0 = gy * j->th;
     long x1 = x0 + j->tw, y1 = y0 + j->th;
@@ -172,14 +174,16 @@ static void *tile_worker(void *arg) {
   return NULL;
 }
 
-static void run_tiles(step_ctx *c, const double *u, double *un, long tiles_x,
-                      long tiles_y, int nthreads) {
+static void run_tiles_n(step_ctx *c, const double *u, double *un, long tiles_x,
+                        long tiles_y, long first, long ntiles, int nthreads) {
   tile_job j;
   j.c = c;
   j.u = u;
   j.un = un;
   j.tiles_x = tiles_x;
   j.tiles_y = tiles_y;
+  j.first = first;
+  j.ntiles = ntiles;
   j.tw = (c->p->nx + tiles_x - 1) / tiles_x;
   j.th = (c->p->ny + tiles_y - 1) / tiles_y;
   j.next_tile = 0;
@@ -193,6 +197,11 @@ static void run_tiles(step_ctx *c, const double *u, double *un, long tiles_x,
     free(th);
   }
   pthread_mutex_destroy(&j.mu);
+}
+
+static void run_tiles(step_ctx *c, const double *u, double *un, long tiles_x,
+                      long tiles_y, int nthreads) {
+  run_tiles_n(c, u, un, tiles_x, tiles_y, 0, tiles_x * tiles_y, nthreads);
 }
 
 void nlh_oracle_step(const nlh_oracle_params *p, long t, const double *u,
@@ -263,6 +272,29 @@ double nlh_oracle_run_tiled(const nlh_oracle_params *p, long nt, long tiles_x,
   }
   clock_gettime(CLOCK_MONOTONIC, &t1);
   if (cur != u) memcpy(u, cur, sizeof(double) * n);
+  ctx_free(&c);
+  free(b);
+  return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}
+
+/* Timing sample of run_tiled's step t on a lattice too large to step whole
+ * within the CPU baseline's budget: tiles first .. first+ntiles-1 (row-major)
+ * of the same lattice, same tiling and threads; seconds.  The rest of the
+ * next field is left uncomputed (it is only a timing). */
+double nlh_oracle_time_tiles(const nlh_oracle_params *p, long t, long tiles_x, long tiles_y,
+                             long first, long ntiles, const double *u, int nthreads) {
+  const size_t n = (size_t)(p->nx * p->ny);
+  double *b = (double *)calloc(n ? n : 1, sizeof(double));
+  step_ctx c;
+  ctx_init(&c, p);
+  ctx_time(&c, t);
+  if (first < 0) first = 0;
+  if (first > tiles_x * tiles_y) first = tiles_x * tiles_y;
+  if (ntiles > tiles_x * tiles_y - first) ntiles = tiles_x * tiles_y - first;
+  struct timespec t0, t1;
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+  run_tiles_n(&c, u, b, tiles_x, tiles_y, first, ntiles, nthreads);
+  clock_gettime(CLOCK_MONOTONIC, &t1);
   ctx_free(&c);
   free(b);
   return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);

@@ -76,6 +76,9 @@ void nlh_oracle_errors(const nlh_oracle_params *p, long time, const double *u,
  * results.  Returns the wall time in seconds of the nt-step loop.           */
 double nlh_oracle_run_tiled(const nlh_oracle_params *p, long nt, long tiles_x,
                             long tiles_y, double *u, int nthreads);
+/* one step (index t) of run_tiled over only tiles first .. first+ntiles-1 (timing sample); seconds */
+double nlh_oracle_time_tiles(const nlh_oracle_params *p, long t, long tiles_x, long tiles_y,
+                             long first, long ntiles, const double *u, int nthreads);
 
 /* ---- 1D solver (src/1d_nonlocal_serial.cpp) --------------------------------
  * c_1d is declared `long` in the reference (1d :57,74): (k*3)/pow(eps*dx,3) is

@@ -58,6 +58,9 @@ def lib() -> ctypes.CDLL:
         L.nlh_oracle_errors.argtypes = [P, ctypes.c_long, dp, dp, dp]
         L.nlh_oracle_run_tiled.argtypes = [P, ctypes.c_long, ctypes.c_long, ctypes.c_long, dp, ctypes.c_int]
         L.nlh_oracle_run_tiled.restype = ctypes.c_double
+        L.nlh_oracle_time_tiles.argtypes = [P, ctypes.c_long, ctypes.c_long, ctypes.c_long, ctypes.c_long,
+                                            ctypes.c_long, dp, ctypes.c_int]
+        L.nlh_oracle_time_tiles.restype = ctypes.c_double
         L.nlh_oracle_c1d.argtypes = [ctypes.c_long, ctypes.c_double, ctypes.c_double]
         L.nlh_oracle_c1d.restype = ctypes.c_double
         L.nlh_oracle_run_1d.argtypes = [ctypes.c_long, ctypes.c_long, ctypes.c_long, ctypes.c_double,
@@ -128,6 +131,16 @@ def run_tiled(p: Params, nt: int, tiles_x: int, tiles_y: int, u: np.ndarray, nth
     """In-place tiled run (2d_nonlocal_async execution model); returns seconds."""
     assert u.dtype == np.float64 and u.flags.c_contiguous
     return lib().nlh_oracle_run_tiled(ctypes.byref(p), int(nt), int(tiles_x), int(tiles_y), _dp(u), int(nthreads))
+
+
+def time_tiles(p: Params, t: int, tiles_x: int, tiles_y: int, first: int, ntiles: int, u: np.ndarray,
+               nthreads: int) -> float:
+    """Seconds of run_tiled's step t over only tiles first .. first+ntiles-1
+    (row-major; a bounded timing sample of a lattice too large to step whole);
+    u is not changed."""
+    assert u.dtype == np.float64 and u.flags.c_contiguous
+    return lib().nlh_oracle_time_tiles(ctypes.byref(p), int(t), int(tiles_x), int(tiles_y), int(first), int(ntiles),
+                                       _dp(u), int(nthreads))
 
 
 # ---- 1D solver (src/1d_nonlocal_serial.cpp) ---------------------------------

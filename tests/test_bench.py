@@ -62,3 +62,16 @@ def test_multi_gpu_line_fields():
     assert bad["strong_efficiency"] is None and bad["strong_reference"] == {"error": "boom"}
     # one GPU without a communicator
     assert bench.scaling_fields(1, False, 1.0) == {"nranks_seen": 1}
+
+
+def test_cpu_baseline_bounded_sample():
+    """The CPU baseline stays bounded on lattices whose whole step exceeds its
+    budget (C4's 8192^2 at eps 32: ~2 min per step on the GPU box's host
+    share): it times the centre tile rows of one step of the same lattice and
+    says so; small workloads still time whole steps.  Both carry the
+    single-core serial leg."""
+    big = bench.cpu_baseline(2, 512, 16, budget_s=0.05, serial_budget_s=0.05)
+    assert big["value"] > 0 and "tile rows of one step" in big["sample"] and "512x512 lattice" in big["sample"]
+    assert big["serial_1core"]["cores"] == 1 and big["serial_1core"]["value"] > 0
+    small = bench.cpu_baseline(2, 256, 2, budget_s=2.0, serial_budget_s=0.05)
+    assert small["value"] > 0 and "step(s)" in small["sample"]
