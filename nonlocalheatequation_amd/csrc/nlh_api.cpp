@@ -889,7 +889,8 @@ int compute_lw(nlh_solver *s) {
   const int ext = s->pair ? (int)s->p.eps : 0;
   for (auto &b : s->blocks) {
     double *tmp = b.base[1];
-    if (nlh::launch_fill_w0(tmp, b.pitch, b.xl, (int)b.r.w, (int)b.r.h, s->halo, (int)b.r.x0,
+    // the whole buffer: rows above the block as origin() counts them
+    if (nlh::launch_fill_w0(tmp, b.pitch, b.xl, (int)b.r.w, (int)b.r.h, (int)((b.rows - b.r.h) / 2), (int)b.r.x0,
                             (int)b.r.y0, s->sc, s->s_main))
       return fail(NLH_ERR_HIP, "fill_w0 launch");
     nlh::RectList rl{};

@@ -43,6 +43,17 @@ namespace nlh {
 
 constexpr int kPairSplitD = 8;  // k_pair_split: rows in flight beyond the next block
 constexpr int kPairSplitB = 4;  // k_pair_split: rows per barrier
+// k_pair_split code-shape options (results bitwise identical): 1 = the output
+// row pointer advances by one row per iteration (no 64-bit row multiply and
+// fewer scalar instructions per store); 2 = unclamped row DMA (the ring's
+// tail DMAs, at most 2B + D rows past a segment's last input row, read
+// kPairPadRows padding rows beyond the halo -- only the tools/ harness
+// allocates them).  C2 harness, three boxes (profiles/r04/{pairopt,eighth}): per
+// pass 75.8 us without, 74.3 with 1, 75.1 with 2, 74.9 with both -- option 1
+// in production.  E = 13 keeps the multiply: with option 1 hipcc 7.2
+// allocates 256 VGPRs and spills 76-116 bytes there (230 / 242 without)
+constexpr int kPairPadRows = 16;
+__host__ __device__ constexpr int pair_opt(int E) { return E == 13 ? 0 : 1; }
 
 // some row offset d of the disk has half-width len(d) == L
 __host__ __device__ constexpr bool pair_level_used(int E, int L) {
@@ -182,7 +193,7 @@ __device__ __forceinline__ void pair_scatter(const double (&w)[2 * E + 2], doubl
 // stage 2 folds that into the centre accumulator of the same row, so
 // u^{t+2} = alpha*(S + kc u^{t+1} + (dt/alpha) b(t+1)).  L_h[W0] is read once
 // per two steps.
-template <int E, int D, int ABL = 0, int B = kPairSplitB, bool TEST = false>
+template <int E, int D, int ABL = 0, int B = kPairSplitB, bool TEST = false, int OPT = pair_opt(E)>
 __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) {
   constexpr int R = 2;
   constexpr int P = pair_slots(E);      // accumulator slots = rows per unrolled period
@@ -208,6 +219,7 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
   static_assert(D * GA + D + 1 < 64, "vmcnt range");
   static_assert(WO >= 64, "strip too narrow for this eps");
   static_assert(P <= 2 * E + B, "the peeled iterations 0 .. P-1 carry no u^{t+1} row");
+  static_assert((OPT & 2) == 0 || 2 * B + D <= kPairPadRows, "tail DMAs past the padding rows");
 
   __shared__ __attribute__((aligned(16))) double ring[K * RW + U1R * U1W + (TEST ? U1R * U1W + K * LWW + 2 * K : 0)];
   double *const u1buf = ring + K * RW;
@@ -341,7 +353,7 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
     const int yfirst = up ? (Y1 + 2 * E - 1) : (Y0 - 2 * E);
     const double *gnext = Rc.u + (int64_t)yfirst * pitch + (x0 - 2 * E);
     const uint32_t lring = __builtin_amdgcn_readfirstlane(lds_addr(ring));
-    int row = 0;  // next u^t row to fetch (clamped at the last one)
+    [[maybe_unused]] int row = 0;  // next u^t row to fetch (clamped at the last one; OPT & 2: unused)
     int irow = 0;  // u^t row index of the next issue (unclamped; TEST rows follow it)
     const double *lw0p = TEST ? Rc.lw + (x0 - E - LOFF) : nullptr;
     const uint32_t llw = __builtin_amdgcn_readfirstlane(lds_addr(lwr));
@@ -364,8 +376,8 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
         dma_chunks<NCH>(gnext, lring + slot * RW * 8, lane);
       else if (!(ABL & 2) && !(ABL & 256))
         dma_chunks<NCH, false, false>(gnext, lring + slot * RW * 8, lane);
-      if constexpr ((ABL & 32) != 0)
-        gnext += stride;
+      if constexpr ((ABL & 32) != 0 || (OPT & 2) != 0)
+        gnext += stride;  // past the last input row: the block's padding rows
       else if (++row < n_in)
         gnext += stride;
     };
@@ -403,6 +415,9 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
       block_end(i);
     }
     int bs = P & (K - 1);  // b % K
+    // OPT & 1: output row of iteration i (row yout0 + ydir (m2 - 2E)), advanced
+    // by one row per iteration; starts at i = P
+    double *dstp = run + (int64_t)(yout0 + ydir * (P - 4 * E - B)) * pitch;
     for (int b = P; b <= i_last; b += P) {
       auto body = [&](auto qc) {
         constexpr int q = decltype(qc)::value;
@@ -427,7 +442,7 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
         if ((ABL & 32) != 0 || m2 >= 2 * E) {
           const double o0 = alpha * acc[0][so];
           const double o1 = alpha * acc[1][so];
-          double *dst = run + (int64_t)(yout0 + ydir * (m2 - 2 * E)) * pitch;
+          double *dst = (OPT & 1) ? dstp : run + (int64_t)(yout0 + ydir * (m2 - 2 * E)) * pitch;
           if constexpr ((ABL & 2) != 0 || (ABL & 128) != 0) {
             asm volatile("" ::"v"(o0), "v"(o1));
           } else if constexpr ((ABL & 512) != 0) {  // ablation: non-temporal stores
@@ -443,12 +458,13 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
             dst[xo] = o0;
           }
         }
+        if constexpr ((OPT & 1) != 0) dstp += stride;
         if constexpr ((ABL & 40) != 40) block_end(i);
       };
       static_for<P>(body);
       bs = (bs + P) & (K - 1);
     }
-    wait_vmcnt<0>();  // drain the clamped tail DMAs and the stores
+    wait_vmcnt<0>();  // drain the tail DMAs and the stores
   }
 }
 

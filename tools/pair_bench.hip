@@ -47,7 +47,7 @@ int main(int argc, char **argv) {
   const int seg_force = argc > 3 ? std::atoi(argv[3]) : 0;
   const int H = 2 * E, XL = 16;
   const int64_t pitch = ((XL + std::max<int64_t>(ceil_div(n, 256) * 256 + XL, n + 128)) + 7) / 8 * 8;
-  const int64_t rows = n + 2 * H;
+  const int64_t rows = n + 2 * (H + kPairPadRows);  // the library's pair-solver block layout
   const size_t bytes = (size_t)(pitch * rows) * sizeof(double);
   double *buf[2];
   for (auto &b : buf) {
@@ -59,7 +59,7 @@ int main(int argc, char **argv) {
   for (int y = 0; y < n; ++y)
     for (int x = 0; x < n; ++x) h[(size_t)y * n + x] = std::sin(2 * M_PI * (x * dh)) * std::sin(2 * M_PI * (y * dh)) +
                                                       0.25 * std::sin(2 * M_PI * (7 * x * dh + 3 * y * dh));
-  auto origin = [&](double *b) { return b + (int64_t)H * pitch + XL; };
+  auto origin = [&](double *b) { return b + (int64_t)(H + kPairPadRows) * pitch + XL; };
   int disk = 0;
   for (int d = -E; d <= E; ++d) disk += 2 * clen(E, d < 0 ? -d : d) + 1;
   StepConst C{};
@@ -82,11 +82,15 @@ int main(int argc, char **argv) {
   // 8 no s_barrier, 16 no u^{t+1} LDS writes, 32 no checks, 64 no vmcnt
   // wait, 128 no store, 256 no DMA, 512 nt stores, 1024 nt DMA; 452 = VALU
   // only (no LDS reads, no vmcnt waits, no stores, no DMA)
+  // OPT (nlh_pair.h): 1 incremental output row pointer, 2 unclamped row DMA
   std::vector<Variant> vs = {
-      {"rows_D4_B2", k_pair_split<E, 4, 0, 2>, 128, 4, 128 - 2 * E},
-      {"rows_D8_B4", k_pair_split<E, 8, 0, 4>, 128, 4, 128 - 2 * E},
-      {"rows_D4_B2_b", k_pair_split<E, 4, 0, 2>, 128, 4, 128 - 2 * E},
-      {"rows_D8_B4_b", k_pair_split<E, 8, 0, 4>, 128, 4, 128 - 2 * E},
+      {"D4_B2_opt0", k_pair_split<E, 4, 0, 2, false, 0>, 128, 4, 128 - 2 * E},
+      {"D4_B2_opt1", k_pair_split<E, 4, 0, 2, false, 1>, 128, 4, 128 - 2 * E},
+      {"D4_B2_opt2", k_pair_split<E, 4, 0, 2, false, 2>, 128, 4, 128 - 2 * E},
+      {"D4_B2_opt3", k_pair_split<E, 4, 0, 2, false, 3>, 128, 4, 128 - 2 * E},
+      {"D4_B2_opt0_b", k_pair_split<E, 4, 0, 2, false, 0>, 128, 4, 128 - 2 * E},
+      {"D4_B2_opt3_b", k_pair_split<E, 4, 0, 2, false, 3>, 128, 4, 128 - 2 * E},
+      {"D8_B4_opt3", k_pair_split<E, 8, 0, 4, false, 3>, 128, 4, 128 - 2 * E},
   };
 
 
