@@ -285,12 +285,17 @@ struct nlh_solver {
   int vranks = 0;       // NLH_VIRTUAL_RANKS count (0: one real rank per process)
   std::vector<int> mine;  // ranks this process runs: {rank}, or 0 .. vranks-1
   int owners = 1;  // owner ids in the tile map: nranks, or NLH_VIRTUAL_RANKS
-  // exchange schedule (profiles/r01/sched): interior workgroups per CU in the
-  // segment model when an exchange runs beside it (RCCL kernels need the LDS
-  // a fourth k_pair_split workgroup would hold; NLH_INT_PER_CU, 0 = all), and
-  // where the bands run (NLH_SCHED): 2 = on the exchange stream (default),
-  // 0 = own stream beside the interior, 1 = before the interior on s_main
-  int int_per_cu = 3;
+  // exchange schedule: interior workgroups per CU in the segment model when
+  // an exchange runs beside it (NLH_INT_PER_CU, 0 = all the pass kernel's
+  // slots), and where the bands run (NLH_SCHED): 2 = on the exchange stream
+  // (default), 0 = own stream beside the interior, 1 = before the interior on
+  // s_main.  Round 4: all slots (0) beat round 1's 3 per CU on one rank's
+  // blocks over RCCL to self -- 4096^2 as 2x1 blocks 82 vs 88-90 us per pass,
+  // 8192x4096 as 2x1 156-157 vs 164-166, 8192^2 as 2x2 290-295 vs 296-298
+  // (profiles/r04/sched); the pass kernel's 4 workgroups per CU hold 252 of
+  // 512 VGPRs per SIMD lane and 56 of 160 KB of LDS, so bands and RCCL
+  // kernels still find room beside them
+  int int_per_cu = 0;
   int sched = 2;
   int64_t t = 0;
   int cur = 0;
@@ -423,9 +428,9 @@ int build_rectlists(nlh_solver *s, int kind) {
         const int per_cu = std::max(1, nlh::pair_blocks_per_cu(E, s->p.test ? s->pair_test : s->pair_split));
         int use_cu = std::min(per_cu, s->pair_cu);
         // with an exchange the interior may be sized for fewer slots per CU,
-        // leaving room for the bands and RCCL beside it (NLH_INT_PER_CU)
-        // -- measured a win up to 4096^2-sized blocks (166 vs 182 us/step for
-        // four 4096^2 blocks over RCCL), a loss on the 16384 x 8192 share of C3
+        // leaving room for the bands and RCCL beside it (NLH_INT_PER_CU; off by
+        // default since round 4, see int_per_cu) -- never on blocks past
+        // 4096 x 8192 (a loss on the 16384 x 8192 share of C3)
         int64_t big = 0;
         for (auto &it : all) big = std::max<int64_t>(big, s->blocks[it.blk].r.w * s->blocks[it.blk].r.h);
         if (s->exchange_planned && s->int_per_cu > 0 && big <= (int64_t)4096 * 8192)
