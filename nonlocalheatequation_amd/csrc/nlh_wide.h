@@ -138,7 +138,7 @@ __device__ __forceinline__ double wave_prefix_sum(double x) {
 // taps instead of running alone.  Same arithmetic: bitwise equal.
 template <int E, int CH, bool TEST, int D = kWideD, int ABL = 0, int PIN = 1, bool AB = false, int OBP = 16,
           bool SPLIT8 = true, bool PS = false, int PA = 0, bool PSPLIT = false, bool ILS = false, bool NTS = false,
-          bool RP = false>
+          bool RP = false, bool SP = false>
 __global__ __launch_bounds__(64, 1) void k_wide(RectList L, StepConst C) {
   constexpr int W = 64;                 // output columns per strip
   constexpr int EP = (E + 1) & ~1;      // staged halo columns per side (16-B rows)
@@ -531,12 +531,17 @@ __global__ __launch_bounds__(64, 1) void k_wide(RectList L, StepConst C) {
     static_for<CH>(row);
     // outputs a = 0 .. CH-1 complete: k = ibase - 2E + a
     full = ibase - 2 * E >= 0 && ibase - 2 * E + CH <= nout;
+    // SP: one 64-bit row multiply per chunk; the CH stores step a row pointer
+    // (ISA: 19 scalar instructions per store with the multiply each, E = 32)
+    double *op = SP ? run + (int64_t)(up ? Y1 - 1 - (ibase - 2 * E) : Y0 + (ibase - 2 * E)) * pitch : nullptr;
     auto store = [&](auto ac) __attribute__((always_inline)) {
       constexpr int a = decltype(ac)::value;
       const int k = ibase - 2 * E + a;
+      double *const orow = op;
+      if constexpr (SP) op += stride;
       if (k < 0 || k >= nout) return;
       if (emit) {
-        double *dst = run + (int64_t)(up ? Y1 - 1 - k : Y0 + k) * pitch + xl;
+        double *dst = SP ? orow + xl : run + (int64_t)(up ? Y1 - 1 - k : Y0 + k) * pitch + xl;
         if constexpr (NTS)
           __builtin_nontemporal_store(alpha * acc[a], dst);  // NTS: streaming store (tools/ harness)
         else
@@ -592,10 +597,13 @@ constexpr bool wide_ils() { return wide_pa<E>() > 0; }
 template <int E, bool TEST>
 constexpr bool wide_rp() { return !TEST && (wide_pa<E>() > 0 || E > 40); }
 
+// ... and the chunk's output row pointer (SP) instead of a 64-bit row multiply
+// per store: C4 398-402 -> 391-397 us per step in tools/wide_bench.hip, bitwise
+// equal, same registers at every E (profiles/r04/widesp)
 template <int E, bool TEST>
 int launch_wide_e(const RectList &rl, const StepConst &c, hipStream_t st) {
   hipLaunchKernelGGL((k_wide<E, wide_chunk_pa<E>(), TEST, kWideD, 0, 1, false, 16, true, wide_ps<E>(), wide_pa<E>(),
-                             (wide_pa<E>() > 0), wide_ils<E>(), wide_ils<E>(), wide_rp<E, TEST>()>),
+                             (wide_pa<E>() > 0), wide_ils<E>(), wide_ils<E>(), wide_rp<E, TEST>(), true>),
                      dim3(rl.nwork), dim3(64), 0, st, rl, c);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : (int)e;
@@ -608,7 +616,7 @@ int wide_blocks_per_cu_e() {
   int n = 0;
   const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
       &n, k_wide<E, wide_chunk_pa<E>(), false, kWideD, 0, 1, false, 16, true, wide_ps<E>(), wide_pa<E>(),
-             (wide_pa<E>() > 0), wide_ils<E>(), wide_ils<E>(), wide_rp<E, false>()>,
+             (wide_pa<E>() > 0), wide_ils<E>(), wide_ils<E>(), wide_rp<E, false>(), true>,
       64, 0);
   return e == hipSuccess ? n : 0;
 }

@@ -80,23 +80,16 @@ int main(int argc, char **argv) {
   // variants: prefix-sum rows (production, PA = 0) and prefix rows built PA
   // rows ahead (k_wide PA), at DMA depths 6 and 8
 #if WB_E <= 32
-  // production (WPG 1: one wave per 64-column strip, nt DMA) vs shared staged
-  // rows (WPG waves per workgroup over one 64 WPG + 2 EP row) and the DMA's
-  // cache policy (DNT)
-#define KW(WPG, DNT) k_wide<E, 8, false, 6, 0, 1, false, 16, true, true, 2, true, true, true, true, WPG, DNT>
+  // production form (prefix rows two ahead, interleaved scan, row pairs) with
+  // the per-store row multiply vs the chunk's row pointer (SP)
+#define KW(SP) k_wide<E, 8, false, 6, 0, 1, false, 16, true, true, 2, true, true, true, true, SP>
   std::vector<Variant> vs = {
-      {"prod_wpg1_nt", KW(1, true), 64, 8, 64},
-      {"wpg1_dflt", KW(1, false), 64, 8, 64},
-      {"wpg2_nt", KW(2, true), 128, 4, 128},
-      {"wpg2_dflt", KW(2, false), 128, 4, 128},
-      {"wpg4_nt", KW(4, true), 256, 2, 256},
-      {"wpg4_dflt", KW(4, false), 256, 2, 256},
-      {"prod_wpg1_nt_b", KW(1, true), 64, 8, 64},
-      {"wpg1_dflt_b", KW(1, false), 64, 8, 64},
-      {"wpg2_nt_b", KW(2, true), 128, 4, 128},
-      {"wpg2_dflt_b", KW(2, false), 128, 4, 128},
-      {"wpg4_nt_b", KW(4, true), 256, 2, 256},
-      {"wpg4_dflt_b", KW(4, false), 256, 2, 256},
+      {"prod", KW(false), 64, 8, 64},
+      {"sp", KW(true), 64, 8, 64},
+      {"prod_b", KW(false), 64, 8, 64},
+      {"sp_b", KW(true), 64, 8, 64},
+      {"prod_c", KW(false), 64, 8, 64},
+      {"sp_c", KW(true), 64, 8, 64},
   };
 #else
   // nested windows, 8-row chunks (the production form past eps 35), one row
@@ -104,8 +97,11 @@ int main(int argc, char **argv) {
   std::vector<Variant> vs = {
       {"nested_C8_D6", k_wide<E, 8, false, 6>, 64, 4},
       {"nested_C8_D6_rp", k_wide<E, 8, false, 6, 0, 1, false, 16, true, false, 0, false, false, false, true>, 64, 4},
-      {"nested_C8_D6_b", k_wide<E, 8, false, 6>, 64, 4},
+      {"nested_C8_D6_rp_sp", k_wide<E, 8, false, 6, 0, 1, false, 16, true, false, 0, false, false, false, true, true>,
+       64, 4},
       {"nested_C8_D6_rp_b", k_wide<E, 8, false, 6, 0, 1, false, 16, true, false, 0, false, false, false, true>, 64, 4},
+      {"nested_C8_D6_rp_sp_b", k_wide<E, 8, false, 6, 0, 1, false, 16, true, false, 0, false, false, false, true, true>,
+       64, 4},
   };
 #endif
 
