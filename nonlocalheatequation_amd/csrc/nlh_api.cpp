@@ -1136,7 +1136,9 @@ int create_impl(const nlh_params *pin, nlh_solver *s, ncclComm_t reuse_comm = nu
     const int64_t right = std::max({round_up(b.r.w, 256) + XL, s->pair ? b.r.w + 128 : (int64_t)0,
                                     s->prefix ? round_up(b.r.w, 64) + 512 : (int64_t)0});
     b.pitch = round_up(XL + right, 8) + pitch_pad;
-    b.rows = b.r.h + 2 * s->halo;
+    // pair passes: padding rows beyond the halo rows, above and below, that
+    // k_pair_split's tail row DMAs read instead of clamping (nlh_pair.h)
+    b.rows = b.r.h + 2 * (s->halo + (s->pair ? nlh::pair_pad_rows() : 0));
     b.L = b.r.x0 > 0 || s->force_bands;
     b.Rr = b.r.x0 + b.r.w < p.nx || s->force_bands;
     b.T = b.r.y0 > 0 || s->force_bands;

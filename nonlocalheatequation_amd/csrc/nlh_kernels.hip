@@ -574,6 +574,8 @@ int launch_wide(const RectList &rl, const StepConst &c, bool test, void *stream)
   }
 }
 
+int pair_pad_rows() { return kPairPadRows; }
+
 // Two-step pass (nlh_pair.h), instantiated in nlh_pair_e*.hip for E = 1..16
 #define NLH_PAIR_EXTERN(E) \
   extern template int launch_pair_e<E>(const RectList &, const StepConst &, int, hipStream_t); \

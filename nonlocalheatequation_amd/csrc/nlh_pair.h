@@ -46,14 +46,15 @@ constexpr int kPairSplitB = 4;  // k_pair_split: rows per barrier
 // k_pair_split code-shape options (results bitwise identical): 1 = the output
 // row pointer advances by one row per iteration (no 64-bit row multiply and
 // fewer scalar instructions per store); 2 = unclamped row DMA (the ring's
-// tail DMAs, at most 2B + D rows past a segment's last input row, read
-// kPairPadRows padding rows beyond the halo -- only the tools/ harness
-// allocates them).  C2 harness, three boxes (profiles/r04/{pairopt,eighth}): per
-// pass 75.8 us without, 74.3 with 1, 75.1 with 2, 74.9 with both -- option 1
-// in production.  E = 13 keeps the multiply: with option 1 hipcc 7.2
-// allocates 256 VGPRs and spills 76-116 bytes there (230 / 242 without)
+// tail DMAs, at most 2B + D rows past a segment's last input row, read the
+// kPairPadRows padding rows the host allocates beyond each block's halo rows
+// for pair passes); 4 = the single-column store of an odd-width rect's last
+// lane behind a wave-uniform test.  C2 harness (profiles/r04/{pairopt,
+// eighth,pairopt2}): per pass 75.8 us with none, 74.3-75.5 with 1, 74.7-75.3
+// with 1 + 4, 74.0-75.0 with all three.  E = 13 leaves out 1: with it hipcc
+// 7.2 allocates 256 VGPRs and spills 76-116 bytes there (229 / 242 without)
 constexpr int kPairPadRows = 16;
-__host__ __device__ constexpr int pair_opt(int E) { return E == 13 ? 0 : 1; }
+__host__ __device__ constexpr int pair_opt(int E) { return E == 13 ? 6 : 7; }
 
 // some row offset d of the disk has half-width len(d) == L
 __host__ __device__ constexpr bool pair_level_used(int E, int L) {
@@ -388,6 +389,10 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
     const int xo = x0 + R * lane;
     const bool emit0 = R * lane < WO && xo < rx1;
     const bool emit1 = R * lane < WO && xo + 1 < rx1;
+    // OPT & 4: the lane that stores one column (an odd-width rect's last one)
+    // behind a wave-uniform test, so the common row takes one masked store
+    const bool single = emit0 && !emit1;
+    const bool any_single = __builtin_amdgcn_ballot_w64(single) != 0;
     double *const run = Rc.un;
     const int yout0 = up ? Y1 - 1 : Y0;
     // block end at iteration j: wave 0 next reads rows j+1 .. j+B, so row
@@ -452,6 +457,10 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
             } else if (emit0) {
               __builtin_nontemporal_store(o0, dst + xo);
             }
+          } else if constexpr ((OPT & 4) != 0) {
+            if (emit1) *reinterpret_cast<double2 *>(dst + xo) = make_double2(o0, o1);
+            if (any_single)
+              if (single) dst[xo] = o0;
           } else if (emit1) {
             *reinterpret_cast<double2 *>(dst + xo) = make_double2(o0, o1);
           } else if (emit0) {

@@ -18,4 +18,8 @@ int prefix_rt_strip_width(int E);
 void prefix_rt_table(int E, const int32_t *lens, int32_t *out);
 int launch_prefix_rt(const RectList &rl, const StepConst &c, const void *table, bool test, void *stream);
 
+// rows a pair-pass solver allocates beyond each block's halo rows, above and
+// below (nlh_pair.h kPairPadRows: k_pair_split's tail row DMAs read them)
+int pair_pad_rows();
+
 }  // namespace nlh

@@ -84,13 +84,14 @@ int main(int argc, char **argv) {
   // only (no LDS reads, no vmcnt waits, no stores, no DMA)
   // OPT (nlh_pair.h): 1 incremental output row pointer, 2 unclamped row DMA
   std::vector<Variant> vs = {
-      {"D4_B2_opt0", k_pair_split<E, 4, 0, 2, false, 0>, 128, 4, 128 - 2 * E},
       {"D4_B2_opt1", k_pair_split<E, 4, 0, 2, false, 1>, 128, 4, 128 - 2 * E},
-      {"D4_B2_opt2", k_pair_split<E, 4, 0, 2, false, 2>, 128, 4, 128 - 2 * E},
-      {"D4_B2_opt3", k_pair_split<E, 4, 0, 2, false, 3>, 128, 4, 128 - 2 * E},
-      {"D4_B2_opt0_b", k_pair_split<E, 4, 0, 2, false, 0>, 128, 4, 128 - 2 * E},
-      {"D4_B2_opt3_b", k_pair_split<E, 4, 0, 2, false, 3>, 128, 4, 128 - 2 * E},
-      {"D8_B4_opt3", k_pair_split<E, 8, 0, 4, false, 3>, 128, 4, 128 - 2 * E},
+      {"D4_B2_opt5", k_pair_split<E, 4, 0, 2, false, 5>, 128, 4, 128 - 2 * E},
+      {"D4_B2_opt7", k_pair_split<E, 4, 0, 2, false, 7>, 128, 4, 128 - 2 * E},
+      {"D4_B2_opt1_b", k_pair_split<E, 4, 0, 2, false, 1>, 128, 4, 128 - 2 * E},
+      {"D4_B2_opt5_b", k_pair_split<E, 4, 0, 2, false, 5>, 128, 4, 128 - 2 * E},
+      {"D4_B2_opt7_b", k_pair_split<E, 4, 0, 2, false, 7>, 128, 4, 128 - 2 * E},
+      {"D4_B2_opt1_c", k_pair_split<E, 4, 0, 2, false, 1>, 128, 4, 128 - 2 * E},
+      {"D4_B2_opt5_c", k_pair_split<E, 4, 0, 2, false, 5>, 128, 4, 128 - 2 * E},
   };
 
 
