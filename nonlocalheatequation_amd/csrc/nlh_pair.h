@@ -43,7 +43,7 @@ namespace nlh {
 
 constexpr int kPairSplitD = 8;  // k_pair_split: rows in flight beyond the next block
 constexpr int kPairSplitB = 4;  // k_pair_split: rows per barrier
-// k_pair_split code-shape options (results bitwise identical): 1 = the output
+// k_pair_split code-shape and scheduling options (results bitwise identical): 1 = the output
 // row pointer advances by one row per iteration (no 64-bit row multiply and
 // fewer scalar instructions per store); 2 = unclamped row DMA (the ring's
 // tail DMAs, at most 2B + D rows past a segment's last input row, read the
@@ -52,9 +52,14 @@ constexpr int kPairSplitB = 4;  // k_pair_split: rows per barrier
 // lane behind a wave-uniform test.  C2 harness (profiles/r04/{pairopt,
 // eighth,pairopt2}): per pass 75.8 us with none, 74.3-75.5 with 1, 74.7-75.3
 // with 1 + 4, 74.0-75.0 with all three.  E = 13 leaves out 1: with it hipcc
-// 7.2 allocates 256 VGPRs and spills 76-116 bytes there (229 / 242 without)
+// 7.2 allocates 256 VGPRs and spills 76-116 bytes there (229 / 242 without).
+// 8 = wave 1 (DMA + stage 2 + stores, the longer of the two lockstep roles)
+// at wave priority 3 (s_setprio), so a SIMD holding it beside another
+// workgroup's stage-1 wave issues it first: C2 harness 73.3-74.9 -> 71.5-72.8
+// us per pass, bitwise equal (priority 1 / 2: 71.7-73.0 / 72.3-72.7;
+// wave 0 first instead: 73.5-74.1; profiles/r04/prio/)
 constexpr int kPairPadRows = 16;
-__host__ __device__ constexpr int pair_opt(int E) { return E == 13 ? 6 : 7; }
+__host__ __device__ constexpr int pair_opt(int E) { return E == 13 ? 14 : 15; }
 
 // some row offset d of the disk has half-width len(d) == L
 __host__ __device__ constexpr bool pair_level_used(int E, int L) {
@@ -287,6 +292,8 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
 
   // barriers: one prologue barrier, then one after every iteration i with
   // i % B == B-1, for i = 0 .. i_last (wave 0 stops computing at n_in - 1)
+  if constexpr ((OPT & 8) != 0)
+    if (wave == 1) __builtin_amdgcn_s_setprio(3);
   if (wave == 0) {
     // ---- stage 1 on u^t row i
     const int gny = (int)C.ny;
