@@ -82,7 +82,33 @@ int main(int argc, char **argv) {
   // 8 no s_barrier, 16 no u^{t+1} LDS writes, 32 no checks, 64 no vmcnt
   // wait, 128 no store, 256 no DMA, 512 nt stores, 1024 nt DMA; 452 = VALU
   // only (no LDS reads, no vmcnt waits, no stores, no DMA)
-  // OPT (nlh_pair.h): 1 incremental output row pointer, 2 unclamped row DMA
+  // OPT (nlh_pair.h): 1 incremental output row pointer, 2 unclamped row DMA,
+  // 4 uniform single-column store, 8 wave 1 at wave priority 3
+#if defined(PB_SET_PRIO)
+  // -DPB_SET_PRIO: OPT 7 (before) against 15 (wave 1 at priority 3), interleaved
+  std::vector<Variant> vs = {
+      {"opt7", k_pair_split<E, 4, 0, 2, false, 7>, 128, 4, 128 - 2 * E},
+      {"opt15", k_pair_split<E, 4, 0, 2, false, 15>, 128, 4, 128 - 2 * E},
+      {"opt7_b", k_pair_split<E, 4, 0, 2, false, 7>, 128, 4, 128 - 2 * E},
+      {"opt15_b", k_pair_split<E, 4, 0, 2, false, 15>, 128, 4, 128 - 2 * E},
+      {"opt7_c", k_pair_split<E, 4, 0, 2, false, 7>, 128, 4, 128 - 2 * E},
+      {"opt15_c", k_pair_split<E, 4, 0, 2, false, 15>, 128, 4, 128 - 2 * E},
+  };
+#elif defined(PB_SET_DB)
+  // -DPB_SET_DB: DMA depth / rows per barrier under the wave priority
+  std::vector<Variant> vs = {
+      {"D4_B2_o15", k_pair_split<E, 4, 0, 2, false, 15>, 128, 4, 128 - 2 * E},
+      {"D8_B4_o15", k_pair_split<E, 8, 0, 4, false, 15>, 128, 4, 128 - 2 * E},
+      {"D4_B4_o15", k_pair_split<E, 4, 0, 4, false, 15>, 128, 4, 128 - 2 * E},
+      {"D6_B2_o15", k_pair_split<E, 6, 0, 2, false, 15>, 128, 4, 128 - 2 * E},
+      {"D2_B2_o15", k_pair_split<E, 2, 0, 2, false, 15>, 128, 4, 128 - 2 * E},
+      {"D4_B2_o15_b", k_pair_split<E, 4, 0, 2, false, 15>, 128, 4, 128 - 2 * E},
+      {"D8_B4_o15_b", k_pair_split<E, 8, 0, 4, false, 15>, 128, 4, 128 - 2 * E},
+      {"D4_B4_o15_b", k_pair_split<E, 4, 0, 4, false, 15>, 128, 4, 128 - 2 * E},
+      {"D6_B2_o15_b", k_pair_split<E, 6, 0, 2, false, 15>, 128, 4, 128 - 2 * E},
+      {"D2_B2_o15_b", k_pair_split<E, 2, 0, 2, false, 15>, 128, 4, 128 - 2 * E},
+  };
+#else
   std::vector<Variant> vs = {
       {"D4_B2_opt1", k_pair_split<E, 4, 0, 2, false, 1>, 128, 4, 128 - 2 * E},
       {"D4_B2_opt5", k_pair_split<E, 4, 0, 2, false, 5>, 128, 4, 128 - 2 * E},
@@ -93,6 +119,7 @@ int main(int argc, char **argv) {
       {"D4_B2_opt1_c", k_pair_split<E, 4, 0, 2, false, 1>, 128, 4, 128 - 2 * E},
       {"D4_B2_opt5_c", k_pair_split<E, 4, 0, 2, false, 5>, 128, 4, 128 - 2 * E},
   };
+#endif
 
 
 
