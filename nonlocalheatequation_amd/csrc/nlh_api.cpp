@@ -276,6 +276,7 @@ struct nlh_solver {
   // 4 = D=8, B=4 (NLH_PAIR_TEST=0)
   int pair_test = 5;
   int pair_cu = 4;     // split-kernel workgroups per CU the segments are sized for (NLH_PAIR_CU)
+  int64_t pair_resident = 0;  // k_pair_split workgroups the device holds at once (0: not yet asked)
   hipStream_t s_main = nullptr, s_comm = nullptr, s_band = nullptr;
   hipEvent_t ev_ready = nullptr, ev_halo = nullptr, ev_band = nullptr, ev_int = nullptr;
   bool halo_fresh = false;  // the current field's halo holds its neighbours' values
@@ -715,7 +716,15 @@ int launch_pair_lists(nlh_solver *s, RLIter b, RLIter e, hipStream_t st) {
   for (; b != e; ++b) {
     const nlh::RectList &rl = *b;
     if (rl.nwork == 0) continue;
-    const int rc = nlh::launch_pair(rl, s->sc, s->p.test ? s->pair_test : s->pair_split, st);
+    // the wave priority of k_pair_split pays only when every workgroup of the
+    // launch is resident at once (nlh_pair.h kPairNoPrio)
+    int v = s->p.test ? s->pair_test : s->pair_split;
+    if (v == 5 || v == 6) {
+      if (s->pair_resident == 0)
+        s->pair_resident = (int64_t)std::max(1, nlh::pair_blocks_per_cu((int)s->p.eps, v)) * s->cus;
+      if (rl.nwork > s->pair_resident) v |= nlh::kPairNoPrio;
+    }
+    const int rc = nlh::launch_pair(rl, s->sc, v, st);
     if (rc != 0) return fail(NLH_ERR_HIP, std::string("pair launch failed: ") + hipGetErrorString((hipError_t)rc));
   }
   return NLH_OK;

@@ -108,6 +108,8 @@ int pair_strip_width(int E);  // output columns per strip: 128 - 2E
 // variant: k_pair_split's ring configuration (nlh_pair.h: 1 / 6 production,
 // 5 / 4 test mode); all bitwise equal
 int pair_blocks_per_cu(int E, int variant);  // resident workgroups per CU (0 = unknown)
+// or'ed into variant 5 / 6: the same kernel without the wave priority (nlh_pair.h)
+constexpr int kPairNoPrio = 0x100;
 int launch_pair(const RectList &rl, const StepConst &c, int variant, void *stream);
 int launch_exact(const RectList &rl, const StepConst &c, bool test, void *stream);
 // fast path for a non-constant J (influence != 0, eps <= 32): LDS tile of

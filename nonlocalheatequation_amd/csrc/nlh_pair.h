@@ -490,12 +490,18 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
 //   5 test mode, 8-slot rings (D = 4, B = 2)     -- default in test mode
 //   4 test mode, 16-slot rings (D = 8, B = 4)    -- NLH_PAIR_TEST=0 (tuning)
 // All four are the same arithmetic in the same order (bitwise equal fields).
+// kPairNoPrio | 6 or | 5: the same kernel without the wave priority (OPT bit
+// 8), which the host launches when a list has more workgroups than the device
+// holds at once: with several rounds of workgroups the priority costs 1-4%
+// (C2 harness 16384^2 / 32768^2: 982-991 vs 995-998 / 3861-3871 vs 4016-4027
+// us per pass), in one round it gains 4% (4096^2 / 8192^2; profiles/r04/prio/)
 // Resident workgroups per CU (register/LDS-limited) for the host's choice of
 // segment height; 0 for an unknown variant
 template <int E>
 int pair_blocks_per_cu_e(int variant) {
   int n = 0;
   hipError_t e = hipErrorInvalidValue;
+  variant &= ~kPairNoPrio;  // same resources with or without the priority
   if (variant == 1) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_pair_split<E, kPairSplitD>, 128, 0);
   else if (variant == 6) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_pair_split<E, 4, 0, 2>, 128, 0);
   else if (variant == 5)
@@ -507,12 +513,17 @@ int pair_blocks_per_cu_e(int variant) {
 
 template <int E>
 int launch_pair_e(const RectList &rl, const StepConst &c, int variant, hipStream_t st) {
+  constexpr int NP = pair_opt(E) & ~8;
   if (variant == 1)
     hipLaunchKernelGGL((k_pair_split<E, kPairSplitD>), dim3(rl.nwork), dim3(128), 0, st, rl, c);
   else if (variant == 6)
     hipLaunchKernelGGL((k_pair_split<E, 4, 0, 2>), dim3(rl.nwork), dim3(128), 0, st, rl, c);
+  else if (variant == (kPairNoPrio | 6))
+    hipLaunchKernelGGL((k_pair_split<E, 4, 0, 2, false, NP>), dim3(rl.nwork), dim3(128), 0, st, rl, c);
   else if (variant == 5)
     hipLaunchKernelGGL((k_pair_split<E, 4, 0, 2, true>), dim3(rl.nwork), dim3(128), 0, st, rl, c);
+  else if (variant == (kPairNoPrio | 5))
+    hipLaunchKernelGGL((k_pair_split<E, 4, 0, 2, true, NP>), dim3(rl.nwork), dim3(128), 0, st, rl, c);
   else if (variant == 4)
     hipLaunchKernelGGL((k_pair_split<E, kPairSplitD, 0, kPairSplitB, true>), dim3(rl.nwork), dim3(128), 0, st,
                        rl, c);
