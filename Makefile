@@ -18,10 +18,13 @@ INC     := -Iinclude -I$(CSRC)
 HIPFLAGS := --offload-arch=$(ARCH) -O3 $(CXXSTD) -fPIC $(WARN) $(INC) -munsafe-fp-atomics
 HOSTFLAGS := -O2 $(CXXSTD) -fPIC $(WARN) $(INC) -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include
 
-# build identity: hash of every library source, the public header and this
-# Makefile (flags), in sorted path order -- nonlocalheatequation_amd.source_build_id()
-# recomputes it from the tree; tests, smoke() and bench.py compare the two
-BUILD_ID_SRCS := $(sort $(wildcard $(CSRC)/*.hip $(CSRC)/*.h $(CSRC)/*.cpp) include/nlh.h Makefile)
+# build identity: hash of every library and driver source, the public header
+# and this Makefile (flags), in sorted path order --
+# nonlocalheatequation_amd.source_build_id() recomputes it from the tree; tests,
+# smoke() and bench.py compare the two, and every driver binary checks at start
+# that the libnlh it loaded carries the id it was built with
+BUILD_ID_SRCS := $(sort $(wildcard $(CSRC)/*.hip $(CSRC)/*.h $(CSRC)/*.cpp $(CSRC)/drivers/*.cpp \
+                   $(CSRC)/drivers/*.h) include/nlh.h Makefile)
 BUILD_ID := $(shell cat $(BUILD_ID_SRCS) | sha256sum | cut -c1-16)
 
 FAST_UNITS := $(sort $(wildcard $(CSRC)/nlh_fast_e*.hip $(CSRC)/nlh_pair_e*.hip $(CSRC)/nlh_wide_e*.hip))
@@ -74,8 +77,8 @@ $(OBJDIR)/nlh_plan.o: $(CSRC)/nlh_plan.cpp $(CSRC)/nlh_plan.h | $(OBJDIR)
 $(LIBDIR)/libnlh.so: $(LIB_OBJS) | $(LIBDIR)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(LIB_OBJS) -L$(ROCM)/lib -lrccl -Wl,-rpath,$(ROCM)/lib
 
-$(OBJDIR)/driver_common.o: $(CSRC)/drivers/driver_common.cpp $(CSRC)/drivers/driver_common.h include/nlh.h | $(OBJDIR)
-	g++ -O2 $(CXXSTD) $(WARN) $(INC) -c $< -o $@
+$(OBJDIR)/driver_common.o: $(CSRC)/drivers/driver_common.cpp $(BUILD_ID_SRCS) | $(OBJDIR)
+	g++ -O2 $(CXXSTD) $(WARN) $(INC) -DNLH_DRIVER_BUILD_ID='"$(BUILD_ID)"' -c $< -o $@
 
 $(OBJDIR)/vtu_writer.o: $(CSRC)/drivers/vtu_writer.cpp $(CSRC)/drivers/vtu_writer.h | $(OBJDIR)
 	g++ -O2 $(CXXSTD) $(WARN) $(INC) -c $< -o $@

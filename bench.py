@@ -38,6 +38,8 @@ import math
 import os
 import socket
 import subprocess
+import tempfile
+import threading
 import sys
 import time
 
@@ -269,12 +271,15 @@ def spawn_ranks(n: int) -> int:
         env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
-                                      stdout=None if r == 0 else subprocess.DEVNULL))
+        outs = tempfile.TemporaryFile(mode="w+")
+        procs.append((subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                       stdout=outs), outs, r))
     # a rank that fails would leave the others blocked in a collective: stop
-    # them (these exact child processes) as soon as one exits non-zero
+    # them (these exact child processes) as soon as one exits non-zero; the
+    # first rank to fail is the one whose error line this launcher prints
     rc = 0
-    live = list(procs)
+    first_bad = None
+    live = [p for p, _, _ in procs]
     while live:
         for p in list(live):
             r = p.poll()
@@ -283,9 +288,28 @@ def spawn_ranks(n: int) -> int:
             live.remove(p)
             if r != 0:
                 rc = max(rc, abs(r))
+                if first_bad is None:
+                    first_bad = p
                 for q in live:
                     q.terminate()
         time.sleep(0.2)
+    lines = {}
+    for p, f, r in procs:
+        f.seek(0)
+        lines[r] = [l for l in f.read().splitlines() if l.startswith("{")]
+        f.close()
+    if rc == 0:
+        for l in lines.get(0, []):
+            print(l, flush=True)
+        return 0
+    bad_rank = next(r for p, _, r in procs if p is first_bad)
+    errs = [l for l in lines.get(bad_rank, []) if '"error"' in l]
+    if errs:
+        print(errs[-1], flush=True)
+    else:
+        code = next(p.returncode for p, _, r in procs if r == bad_rank)
+        print(json.dumps({"error": f"rank {bad_rank} exited with code {code} without an error line",
+                          "rank": bad_rank, "stage": "unknown", "n_gpus": n}), flush=True)
     return rc
 
 
@@ -302,6 +326,65 @@ class stdout_to_stderr:
         sys.stdout.flush()
         os.dup2(self.saved, 1)
         os.close(self.saved)
+
+
+class Stages:
+    """Where a rank is, for the one error line a failed or hung run prints
+    (the first real multi-GPU run must be diagnosable).
+
+    enter(name) starts a watchdog for the stage: if the stage has not ended
+    after its limit (NLH_BENCH_STAGE_TIMEOUT seconds overrides every limit),
+    the rank prints {"error", "rank", "stage", ...} on stdout and exits 124 --
+    ctypes calls release the GIL, so the timer thread runs while the main
+    thread sits in nlh_create / RCCL init / a collective.  fail() prints the
+    same line for an exception or a failed check."""
+    LIMITS = {"process_group": 300, "comm_id": 300, "nlh_create": 900, "comm_check": 300,
+              "first_exchange": 300, "warmup": 900, "timed": 3600, "report": 3600}
+
+    def __init__(self, rank: int, nranks: int):
+        self.rank, self.nranks, self.name, self.timer, self.t0 = rank, nranks, "start", None, time.time()
+        self.lock = threading.Lock()
+        self.done = False
+
+    def line(self, error: str, stage=None) -> str:
+        return json.dumps({"error": error, "rank": self.rank, "stage": stage or self.name,
+                           "n_gpus": self.nranks, "metric": "Gnode-updates/s (nodes*steps/s) fp64",
+                           "elapsed_s": round(time.time() - self.t0, 3)})
+
+    def _expired(self, name: str, limit: float) -> None:
+        with self.lock:
+            if self.done or self.name != name:
+                return
+            self.done = True
+        sys.stderr.flush()
+        os.write(1, (self.line(f"stage '{name}' did not finish within {limit:g} s (hung: a peer rank, the RCCL "
+                               f"rendezvous or a collective)", name) + "\n").encode())
+        os._exit(124)
+
+    def enter(self, name: str) -> None:
+        with self.lock:
+            if self.timer is not None:
+                self.timer.cancel()
+            self.name = name
+            env = os.environ.get("NLH_BENCH_STAGE_TIMEOUT")
+            limit = float(env) if env else float(self.LIMITS.get(name, 3600))
+            self.timer = threading.Timer(limit, self._expired, args=(name, limit))
+            self.timer.daemon = True
+            self.timer.start()
+        if os.environ.get("NLH_BENCH_HANG_STAGE") == name:  # test hook: tests/test_bench.py
+            time.sleep(1e6)
+
+    def end(self) -> None:
+        with self.lock:
+            self.done = True
+            if self.timer is not None:
+                self.timer.cancel()
+
+    def fail(self, error: str, code: int) -> int:
+        self.end()
+        print(self.line(error), flush=True)
+        print(f"rank {self.rank}: {self.name}: {error}", file=sys.stderr, flush=True)
+        return code
 
 
 def strong_reference(args) -> dict:
@@ -405,7 +488,15 @@ def main() -> int:
         print(f"--gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
         return 2
     nranks = world
+    st = Stages(rank, nranks)
+    try:
+        return _run(args, st, rank, local, nranks)
+    except Exception as e:  # noqa: BLE001 -- every failure ends in the one error line
+        return st.fail(f"{type(e).__name__}: {e}", 1)
 
+
+def _run(args, st: Stages, rank: int, local: int, nranks: int) -> int:
+    eps, nb = args.eps, args.lattice
     # strong scaling: the 1-GPU time of the same lattice, before any GPU call here
     t1 = strong_reference(args) if args.strong and nranks > 1 and rank == 0 else None
 
@@ -417,28 +508,24 @@ def main() -> int:
     import nonlocalheatequation_amd as N
     build_id = N.build_id()
     if build_id != N.source_build_id():
-        print(f"libnlh build {build_id} does not match the sources ({N.source_build_id()}): make lib",
-              file=sys.stderr)
-        return 4
+        return st.fail(f"libnlh build {build_id} does not match the sources ({N.source_build_id()}): make lib", 4)
 
     dist = None
     if nranks > 1:
+        st.enter("process_group")
         import torch.distributed as dist  # control plane only (id broadcast, barrier, max)
         dist.init_process_group("gloo")
         if dist.get_world_size() != args.gpus:
-            print(f"process group has {dist.get_world_size()} ranks, expected {args.gpus}", file=sys.stderr)
-            return 3
+            return st.fail(f"process group has {dist.get_world_size()} ranks, expected {args.gpus}", 3)
 
     px, py = decomposition(nranks)
     if args.blocks:
         px, py = (int(v) for v in args.blocks.lower().split("x"))
         if nranks > 1 and px * py != nranks:
-            print(f"--blocks {args.blocks} needs one block per rank", file=sys.stderr)
-            return 2
+            return st.fail(f"--blocks {args.blocks} needs one block per rank", 2)
     if args.strong:
         if nb % px or nb % py:
-            print(f"--lattice {nb} is not divisible by the {px}x{py} block grid", file=sys.stderr)
-            return 2
+            return st.fail(f"--lattice {nb} is not divisible by the {px}x{py} block grid", 2)
         nx, ny = nb, nb
     else:
         nx, ny = nb * px, nb * py
@@ -449,10 +536,12 @@ def main() -> int:
 
     comm_id = None
     if nranks > 1:
+        st.enter("comm_id")
         obj = [N.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         comm_id = obj[0]
 
+    st.enter("nlh_create")  # device, blocks and (N > 1) the RCCL communicator init
     with stdout_to_stderr():
         s = N.Solver(nx, ny, eps, 1.0, dt, dh, test=args.test_mode, kernel=args.kernel, device=local,
                      rank=rank, nranks=nranks, tiles=(px, py), comm_id=comm_id, seg_rows=args.seg_rows,
@@ -464,25 +553,31 @@ def main() -> int:
     # take part
     comm_seen = None
     if dist is not None:
+        st.enter("comm_check")
         lst = [None] * nranks
         dist.all_gather_object(lst, (info.owned_nodes, info.nblocks, info.comm_nranks, info.comm_rank))
         owned = [o[0] for o in lst]
         if sum(owned) != nx * ny or any(o == 0 for o in owned):
-            print(f"ranks own {owned} nodes of {nx * ny}", file=sys.stderr)
-            return 3
+            return st.fail(f"ranks own {owned} nodes of {nx * ny}", 3)
         counts = {o[2] for o in lst}
         ranks_seen = sorted(o[3] for o in lst)
         if counts != {nranks} or ranks_seen != list(range(nranks)):
-            print(f"RCCL communicator sizes {sorted(counts)} / ranks {ranks_seen}, expected {nranks} ranks",
-                  file=sys.stderr)
-            return 5
+            return st.fail(f"RCCL communicator sizes {sorted(counts)} / ranks {ranks_seen}, expected {nranks} "
+                           f"ranks", 5)
         comm_seen = nranks
     s.test_init()
+    # the first pass(es): the first ghost exchange over RCCL on N > 1
+    st.enter("first_exchange")
+    s.run(max(1, info.steps_per_pass))
+    s.synchronize()
+    if dist is not None:
+        dist.barrier()
     # warm-up: W steps, then more until --warmup-ms of stepping has passed (the
     # clocks a sustained run holds); every rank runs the same count (rank 0's)
+    st.enter("warmup")
     s.run(args.warmup)
     s.synchronize()
-    warm = args.warmup
+    warm = args.warmup + max(1, info.steps_per_pass)
     tw = time.perf_counter()
     chunk = max(2, args.warmup)
     while warm < 100000:
@@ -504,6 +599,7 @@ def main() -> int:
             dist.barrier()
 
     barrier()
+    st.enter("timed")
     if rank == 0:
         progress(f"warm-up done ({warm} steps); timing {args.steps} steps")
     # HIP events on the stencil stream bracket the timed region (one pair);
@@ -523,6 +619,7 @@ def main() -> int:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    st.enter("report")
     l2 = s.compute_l2(s.step_index) if args.test_mode else None  # after the timed region
 
     # exchange report (several owners): a separate, untimed run with an event
@@ -663,6 +760,7 @@ def main() -> int:
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+    st.end()
     return 0
 
 

@@ -67,10 +67,19 @@ enum nlh_influence { NLH_INFLUENCE_CONSTANT = 0, NLH_INFLUENCE_LINEAR = 1 };
  * and 36..64 (compile-time k_wide instances), prefix-sum windows for 17..35
  * (k_wide), and past 64 a run-time-horizon prefix-window kernel (k_prefix_rt);
  * in test mode the manufactured source comes from a precomputed L_h[W0]
- * field.  FAST differs from the reference only by summation rounding
- * (<= 1e-12 of field scale per node, L2 error within 1e-10).  AUTO = FAST
- * (production and test mode), EXACT when FAST cannot apply (k*dt*dh = 0
- * past eps 16).                                                           */
+ * field; J = 1 - r runs LDS-tile kernels (k_weighted*) up to eps 52.
+ * FAST differs from the reference only by summation rounding: <= 1e-12 of
+ * field scale at every node.  The L2 error (test mode) then matches to
+ * 1e-10 relative wherever the reference's own error is above the rounding
+ * floor those node differences set (Cauchy-Schwarz bound B = 2 sqrt(l2 S)
+ * + S, S = sum of squared node differences, below 1e-10 l2: every row of
+ * the reference's tests/2d.txt and 2d_async.txt); where the reference's
+ * error is itself at that floor (l2 ~ 1e-20 .. 1e-11: few steps, large
+ * eps) the L2 difference is bounded by B instead.
+ * AUTO = FAST (production and test mode) except where FAST cannot apply,
+ * which runs EXACT: k*dt*dh = 0 past eps 16; eps > 224 (the run-time
+ * kernel's 512-column staged window); J = 1 - r past eps 52 (the weighted
+ * tile past 160 KB of LDS).  An explicit FAST request there is refused.  */
 enum nlh_kernel { NLH_KERNEL_AUTO = 0, NLH_KERNEL_EXACT = 1, NLH_KERNEL_FAST = 2 };
 
 typedef struct nlh_params {

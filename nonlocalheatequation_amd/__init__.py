@@ -169,11 +169,11 @@ def build_id() -> str:
 
 def source_build_id(root: str = _ROOT) -> str:
     """The build identity a library built from the tree at `root` carries:
-    sha256 over the library sources, include/nlh.h and the Makefile in sorted
-    path order, first 16 hex digits (Makefile BUILD_ID)."""
+    sha256 over the library and driver sources, include/nlh.h and the
+    Makefile in sorted path order, first 16 hex digits (Makefile BUILD_ID)."""
     csrc = os.path.join("nonlocalheatequation_amd", "csrc")
     rel = []
-    for pat in ("*.hip", "*.h", "*.cpp"):
+    for pat in ("*.hip", "*.h", "*.cpp", os.path.join("drivers", "*.cpp"), os.path.join("drivers", "*.h")):
         rel += [os.path.relpath(f, root) for f in glob.glob(os.path.join(root, csrc, pat))]
     rel += [os.path.join("include", "nlh.h"), "Makefile"]
     h = hashlib.sha256()

@@ -88,6 +88,27 @@ uint64_t Options::as_u64(const std::string &name) const { return std::stoull(val
 double Options::as_double(const std::string &name) const { return std::stod(vals_.at(name)); }
 
 // ---------------------------------------------------------------- output
+// Every driver links this file: at start, before main, the libnlh the binary
+// loaded must carry the build id the driver was compiled with (Makefile
+// BUILD_ID over the library AND driver sources) -- a stale bin/ driver, or a
+// library rebuilt without relinking the drivers, fails loudly instead of
+// running an old code path.
+#ifndef NLH_DRIVER_BUILD_ID
+#error "compile driver_common.cpp with -DNLH_DRIVER_BUILD_ID (Makefile)"
+#endif
+namespace {
+struct BuildIdCheck {
+  BuildIdCheck() {
+    const char *lib = nlh_build_id();
+    if (!lib || std::strcmp(lib, NLH_DRIVER_BUILD_ID) != 0) {
+      std::fprintf(stderr, "driver built for libnlh %s but loaded libnlh %s: rebuild with `make drivers`\n",
+                   NLH_DRIVER_BUILD_ID, lib ? lib : "(none)");
+      std::exit(3);
+    }
+  }
+} g_build_id_check;
+}  // namespace
+
 void print_banner(const char *argv0) {
   // MAJOR.MINOR.UPDATE of include/Config.h (0.1.0)
   std::cout << argv0 << " (0.1.0)" << std::endl;
@@ -308,7 +329,8 @@ void Logger::log(int64_t t, int64_t vtk_index, const std::vector<double> &u) {
 // ---------------------------------------------------------------- loop
 int run_steps(nlh_solver *s, int64_t nt, int64_t nlog, Logger &lg, bool vtk_index_is_t,
               int rank, uint64_t &elapsed_ns, int nranks, int64_t nbalance,
-              const std::function<int(int64_t)> &on_balance) {
+              const std::function<int(int64_t)> &on_balance, int64_t busy_window,
+              const std::function<int(int64_t)> &on_window) {
   const bool logging = lg.enabled() && nlog > 0;
   // one rank: log steps take an asynchronous snapshot (device copy in stream
   // order, host transfer on a copy stream) and a writer thread formats the
@@ -337,6 +359,15 @@ int run_steps(nlh_solver *s, int64_t nt, int64_t nlog, Logger &lg, bool vtk_inde
       const int64_t from = std::max<int64_t>(t, 1);
       const int64_t next_bal = (from % nbalance == 0) ? from : (from / nbalance + 1) * nbalance;
       last = std::min(last, next_bal);
+      if (busy_window > 0 && on_window) {
+        // the busy window: steps next_bal - busy_window + 1 .. next_bal
+        const int64_t ws = std::max<int64_t>(0, next_bal - busy_window + 1);
+        if (t < ws) {
+          last = std::min(last, ws - 1);
+        } else if (t == ws) {
+          if ((rc = on_window(t)) != NLH_OK) break;
+        }
+      }
     }
     if ((rc = nlh_run(s, last - t + 1)) != NLH_OK) break;
     t = last + 1;

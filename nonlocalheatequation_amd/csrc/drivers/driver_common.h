@@ -101,9 +101,15 @@ void print_errors(double l2, double linf);
 // nbalance > 0: on_balance(t) runs after step t whenever t % nbalance == 0
 // and t != 0 (the reference's load_balance cadence, src/2d_nonlocal_
 // distributed.cpp:1306-1309), before that step's log.
+// busy_window > 0 (with nbalance): on_window(t) runs before step t = the
+// first of the busy_window steps that precede each balance point -- the
+// driver switches busy timing (nlh_kernel_timing mode 2, which serialises a
+// pass's kernels) on there and off again after the balance, so the other
+// steps keep the overlapped exchange schedule.
 int run_steps(nlh_solver *s, int64_t nt, int64_t nlog, Logger &lg, bool vtk_index_is_t,
               int rank, uint64_t &elapsed_ns, int nranks = 1, int64_t nbalance = 0,
-              const std::function<int(int64_t)> &on_balance = {});
+              const std::function<int(int64_t)> &on_balance = {}, int64_t busy_window = 0,
+              const std::function<int(int64_t)> &on_window = {});
 
 // Read the reference's --file partition file (src/2d_nonlocal_distributed.cpp:
 // 467-488): "nx ny npx npy dh" then npx*npy lines "px py owner", px outer.

@@ -19,12 +19,17 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <memory>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "nlh.h"
@@ -40,6 +45,8 @@ int fail(int code, const std::string &msg) {
   g_err = msg;
   return code;
 }
+
+int comm_init_bounded(ncclComm_t *out, int nranks, const ncclUniqueId &id, int rank, int device);
 
 }  // namespace
 
@@ -162,6 +169,7 @@ constexpr EnvKnob kEnvKnobs[] = {
     {"NLH_PAIR_TEST", 0, 1},       // 0: test-mode pass with 16-slot rings
     {"NLH_PITCH_PAD", 0, 1024},    // extra doubles per padded row
     {"NLH_BAND_SEG", 0, 1 << 20},  // edge-band segment height (0 = automatic)
+    {"NLH_COMM_INIT_TIMEOUT", 1, 86400},  // seconds a communicator init may take (default 300)
 };
 constexpr const char *kRemovedKnobs[] = {"NLH_ABLATE", "NLH_PAIR_ABLATE"};
 
@@ -330,7 +338,8 @@ struct nlh_solver {
   double ev_acc_kind[4] = {0.0, 0.0, 0.0, 0.0};  // per EvKind
   std::vector<double> ev_acc_owner;  // folded busy milliseconds per owner
   int64_t timed_steps = 0, timed_passes = 0;  // since timing was enabled
-  double launch_overhead_ms = 0.0;  // busy timing: an empty launch between two events
+  double launch_overhead_ms = 0.0;  // busy timing: the cost of one more (empty) launch in a pair
+  double pair_overhead_ms = 0.0;    // busy timing: an event pair's own cost (once per pair)
   int32_t comm_nranks = 0, comm_rank = -1;  // as RCCL reports them
   int64_t device_bytes = 0;
   char arch[32] = {0};
@@ -1141,9 +1150,10 @@ int create_impl(const nlh_params *pin, nlh_solver *s, ncclComm_t reuse_comm = nu
     b.xl = (int32_t)XL;
     // whole 256-column strips stay in bounds; the pair kernel's last strip
     // stages up to column w + 127
-    // (k_prefix_rt stages 64 NV <= 512 columns from x0 - E of its last strip)
+    // (k_prefix_rt stages 64 NV <= 512 columns from x0 - E of its last strip,
+    // k_prefix_rtc 512-column chunks: prefix_rt_window)
     const int64_t right = std::max({round_up(b.r.w, 256) + XL, s->pair ? b.r.w + 128 : (int64_t)0,
-                                    s->prefix ? round_up(b.r.w, 64) + 512 : (int64_t)0});
+                                    s->prefix ? round_up(b.r.w, 64) + nlh::prefix_rt_window(E) : (int64_t)0});
     b.pitch = round_up(XL + right, 8) + pitch_pad;
     // pair passes: padding rows beyond the halo rows, above and below, that
     // k_pair_split's tail row DMAs read instead of clamping (nlh_pair.h)
@@ -1183,7 +1193,8 @@ int create_impl(const nlh_params *pin, nlh_solver *s, ncclComm_t reuse_comm = nu
     ncclUniqueId id;
     static_assert(sizeof(ncclUniqueId) == NLH_COMM_ID_BYTES, "unique id size");
     std::memcpy(&id, p.comm_id, sizeof(id));
-    NCCL_TRY(ncclCommInitRank(&s->comm, p.nranks, id, p.rank));
+    rc = comm_init_bounded(&s->comm, p.nranks, id, p.rank, s->device);
+    if (rc) return rc;
   } else if (s->rccl_self) {
     ncclUniqueId id;
     NCCL_TRY(ncclGetUniqueId(&id));
@@ -1222,6 +1233,53 @@ int create_impl(const nlh_params *pin, nlh_solver *s, ncclComm_t reuse_comm = nu
     rc = compute_lw(s);
     if (rc) return rc;
   }
+  return NLH_OK;
+}
+
+// ncclCommInitRank with a bounded wait (a first multi-GPU
+// run that hangs in the rendezvous must exit with a diagnosis, not block until
+// the job's time limit).  The init runs on a helper thread (same device); the
+// caller waits up to NLH_COMM_INIT_TIMEOUT seconds (default 300).  On a
+// timeout the helper stays blocked inside RCCL and is detached -- its state is
+// shared, so it never writes to freed memory -- and nlh_create fails with
+// NLH_ERR_RCCL "... timed out"; the process is expected to exit (bench.py
+// prints its error line and does).  The communicator itself stays a blocking
+// one: no call after the init changes.
+struct CommInit {
+  std::mutex m;
+  std::condition_variable cv;
+  bool done = false;
+  ncclResult_t r = ncclInternalError;
+  ncclComm_t comm = nullptr;
+};
+
+int comm_init_bounded(ncclComm_t *out, int nranks, const ncclUniqueId &id, int rank, int device) {
+  int timeout_s = 300;
+  if (const char *v = std::getenv("NLH_COMM_INIT_TIMEOUT"))
+    if (*v) timeout_s = std::atoi(v);
+  auto st = std::make_shared<CommInit>();
+  std::thread th([st, nranks, id, rank, device] {
+    ncclComm_t c = nullptr;
+    ncclResult_t r = hipSetDevice(device) == hipSuccess ? ncclCommInitRank(&c, nranks, id, rank) : ncclUnhandledCudaError;
+    std::lock_guard<std::mutex> lk(st->m);
+    st->comm = c;
+    st->r = r;
+    st->done = true;
+    st->cv.notify_all();
+  });
+  std::unique_lock<std::mutex> lk(st->m);
+  const bool ok = st->cv.wait_for(lk, std::chrono::seconds(timeout_s), [&] { return st->done; });
+  lk.unlock();
+  if (!ok) {
+    th.detach();
+    return fail(NLH_ERR_RCCL, "ncclCommInitRank (rank " + std::to_string(rank) + " of " + std::to_string(nranks) +
+                                  ") timed out after " + std::to_string(timeout_s) +
+                                  " s (NLH_COMM_INIT_TIMEOUT): a peer rank never joined the communicator");
+  }
+  th.join();
+  if (st->r != ncclSuccess)
+    return fail(NLH_ERR_RCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(st->r));
+  *out = st->comm;
   return NLH_OK;
 }
 
@@ -1292,7 +1350,15 @@ int repartition_fits(nlh_solver *s, const std::vector<int32_t> &own) {
     // the vote travels in the solver's own reduction scratch (d_red): the
     // check allocates nothing
     int st = NLH_OK;
-    if (hipMemcpyAsync(s->d_red, &ok, sizeof(double), hipMemcpyHostToDevice, s->s_comm) != hipSuccess) {
+    // a zero vote first: if the upload below fails, this rank still
+    // joins the all-reduce with "does not fit", never with whatever the scratch
+    // held last (an L2 partial that can be >= 1)
+    if (hipMemsetAsync(s->d_red, 0, sizeof(double), s->s_comm) != hipSuccess) {
+      st = fail(NLH_ERR_HIP, "repartition memory check clear");
+      ok = 0.0;
+    }
+    if (st == NLH_OK && ok == 1.0 &&
+        hipMemcpyAsync(s->d_red, &ok, sizeof(double), hipMemcpyHostToDevice, s->s_comm) != hipSuccess) {
       st = fail(NLH_ERR_HIP, "repartition memory check upload");
       ok = 0.0;
     }
@@ -1444,6 +1510,7 @@ int repartition_impl(nlh_solver *s, const std::vector<int32_t> &own) {
   n->halo_fresh = false;
   n->timing = s->timing;
   n->launch_overhead_ms = s->launch_overhead_ms;
+  n->pair_overhead_ms = s->pair_overhead_ms;
   release_impl(s, true);  // the communicator lives on in n
   *s = std::move(*n);
   delete n;  // moved-from shell: its resources now belong to s
@@ -1457,7 +1524,7 @@ int fold_pair(nlh_solver *s, size_t p) {
   HIP_TRY(hipEventElapsedTime(&ms, s->ev_pool[2 * p], s->ev_pool[2 * p + 1]));
   const EvMeta &m = s->ev_meta[p];
   double v = ms;
-  if (m.launches > 0) v = std::max(0.0, v - m.launches * s->launch_overhead_ms);
+  if (m.launches > 0) v = std::max(0.0, v - s->pair_overhead_ms - m.launches * s->launch_overhead_ms);
   s->ev_acc_kind[m.kind] += v;
   if (m.owner >= 0 && m.owner < (int)s->ev_acc_owner.size()) s->ev_acc_owner[m.owner] += v;
   return NLH_OK;
@@ -1864,24 +1931,31 @@ int nlh_kernel_timing(nlh_solver *s, int enable) {
   s->timed_passes = 0;
   s->ev_acc_owner.assign(s->owners, 0.0);
   if (s->timing == 2) {
-    // the fixed cost of one launch between two events (an empty workgroup),
-    // the least of a few tries: subtracted per launch from the busy pairs
-    constexpr int kTries = 8;
-    for (int i = 0; i < kTries; ++i) {
+    // what a busy pair costs beyond its kernels' work: a pair
+    // around ONE empty launch (t1) and around kK of them (tK), the least of a
+    // few tries each; one more launch costs (tK - t1) / (kK - 1), the pair
+    // itself t1 minus one launch -- fold_pair subtracts the pair's cost once
+    // and the launch cost per launch it brackets
+    constexpr int kTries = 8, kK = 8;
+    for (int i = 0; i < 2 * kTries; ++i) {
       const hipEvent_t e0 = pool_event(s), e1 = pool_event(s);
       if (!e0 || !e1) return fail(NLH_ERR_HIP, "event pool");
       HIP_TRY(hipEventRecord(e0, s->s_main));
-      if (nlh::launch_noop(s->s_main)) return fail(NLH_ERR_HIP, "no-op launch");
+      for (int j = 0; j < (i < kTries ? 1 : kK); ++j)
+        if (nlh::launch_noop(s->s_main)) return fail(NLH_ERR_HIP, "no-op launch");
       HIP_TRY(hipEventRecord(e1, s->s_main));
     }
     HIP_TRY(hipStreamSynchronize(s->s_main));
-    float best = 0.f;
-    for (int i = 0; i < kTries; ++i) {
+    float t1 = 0.f, tk = 0.f;
+    for (int i = 0; i < 2 * kTries; ++i) {
       float ms = 0.f;
       HIP_TRY(hipEventElapsedTime(&ms, s->ev_pool[2 * i], s->ev_pool[2 * i + 1]));
-      best = i == 0 ? ms : std::min(best, ms);
+      float &best = i < kTries ? t1 : tk;
+      best = (i == 0 || i == kTries) ? ms : std::min(best, ms);
     }
-    s->launch_overhead_ms = std::max(0.f, best);
+    const double per = std::max(0.0, (double)(tk - t1) / (kK - 1));
+    s->launch_overhead_ms = per;
+    s->pair_overhead_ms = std::max(0.0, (double)t1 - per);
     s->ev_used = 0;
   }
   return NLH_OK;

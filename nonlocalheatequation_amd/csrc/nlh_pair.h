@@ -58,8 +58,30 @@ constexpr int kPairSplitB = 4;  // k_pair_split: rows per barrier
 // workgroup's stage-1 wave issues it first: C2 harness 73.3-74.9 -> 71.5-72.8
 // us per pass, bitwise equal (priority 1 / 2: 71.7-73.0 / 72.3-72.7;
 // wave 0 first instead: 73.5-74.1; profiles/r04/prio/)
+// 16 = the head taps left out: the first period of each stage is peeled, and
+// there a row's taps into output rows that are never emitted (i+d < E) and
+// the nested-window levels only those taps use are skipped (pair_scatter LO;
+// 3.4% fewer f64 adds at C2).  32 = a barrier block's first row also reads
+// the second row's window (B == 2, even period).  64 = 32 and the two rows of
+// a pair build their nested windows in one interleaved instruction stream
+// (pair_levels2 / pair_taps).  All bitwise equal.  C2 harness, the variants
+// interleaved ten times over on one box (profiles/r05/pair_opt/): median per
+// pass 72.48 us (15), 70.41 (15|16|32), 73.37 (15|64), 69.67 (15|16|64).
+// 32 / 64 need ~30 more VGPRs: hipcc spills at E = 13, 14 (test mode), 16,
+// so those take 16 alone; E = 1, 2 have no row pairs.  128 = the tail rows
+// likewise (pair_tail_c: segments of the C2 height only, E = 8), 256 = the
+// stage-1 periods between head and tail without per-row tests (lean).  Where
+// the time goes at C2 (profiles/r05/): eight extra s_nop per row cost 2.4% on
+// the stage-1 wave and nothing on the stage-2 wave -- wave 0 is the critical
+// role under the wave priority, so work off its path pays.  Medians over
+// interleaved repetitions on one box: 15|16|64|128 69.84 us, |256 68.53
+// (E = 8 only: measured there; the lean stage 2 makes hipcc spill).
 constexpr int kPairPadRows = 16;
-__host__ __device__ constexpr int pair_opt(int E) { return E == 13 ? 14 : 15; }
+__host__ __device__ constexpr bool pair_rows(int E);
+__host__ __device__ constexpr int pair_opt(int E) {
+  return E == 8 ? 15 | 16 | 64 | 128 | 256
+                : (E == 13 ? 14 | 16 : (E <= 12 && pair_rows(E) ? 15 | 16 | 64 : 15 | 16));
+}
 
 // some row offset d of the disk has half-width len(d) == L
 __host__ __device__ constexpr bool pair_level_used(int E, int L) {
@@ -115,23 +137,40 @@ __device__ __forceinline__ void pair_window(const double *p, double (&w)[R + 2 *
 // centre term.  ROLE 0: a lone row (no row pairs at this E); 1: row A of a
 // pair (shared taps left to B, its shared levels kept in hs); 2: row B (the
 // pair sums at the shared taps).
-template <int E, int QA, int ROLE>
+// LO (head rows of a segment, OPT & 16): taps at offsets d < LO go to output
+// rows that are never emitted and are left out, and the nested windows are
+// built only up to the largest level a kept tap uses.
+// HI (tail rows of a segment, OPT & 128): likewise for taps at offsets d > HI
+template <int E, int LO, int HI = E>
+__host__ __device__ constexpr int pair_head_lmax() {
+  int m = -1;
+  for (int d = (LO < -E ? -E : LO); d <= (HI > E ? E : HI); ++d)
+    m = clen(E, pair_abs(d)) > m ? clen(E, pair_abs(d)) : m;
+  return m;
+}
+
+template <int E, int QA, int ROLE, int LO = -E, int HI = E>
 __device__ __forceinline__ void pair_scatter(const double (&w)[2 * E + 2], double (&acc)[2][pair_slots(E)],
                                              double kc, double (&hs)[2][E + 1]) {
   constexpr int P = pair_slots(E);
   constexpr int SF = (QA + E) % P;      // d = +E: first term of that output row
   constexpr int SL = (QA + P - E) % P;  // d = -E: last term
-  acc[0][SF] = w[E];
-  acc[1][SF] = w[E + 1];
-  acc[0][SL] += w[E];
-  acc[1][SL] += w[E + 1];
+  constexpr int LMAX = pair_head_lmax<E, LO, HI>();
+  if constexpr (E >= LO && E <= HI) {
+    acc[0][SF] = w[E];
+    acc[1][SF] = w[E + 1];
+  }
+  if constexpr (-E >= LO && -E <= HI) {
+    acc[0][SL] += w[E];
+    acc[1][SL] += w[E + 1];
+  }
   // levels and taps are template constants (static_for): evaluating the
   // disk shape inside the row loop at run time costs more than the sums
   double core = w[E] + w[E + 1];
   auto level = [&](auto lc) {
     constexpr int Lv = decltype(lc)::value + 1;
-    if constexpr (Lv > 1) core = core + (w[E + 1 - Lv] + w[E + Lv]);
-    if constexpr (pair_level_used(E, Lv)) {
+    if constexpr (Lv > 1 && Lv <= LMAX) core = core + (w[E + 1 - Lv] + w[E + Lv]);
+    if constexpr (pair_level_used(E, Lv) && Lv <= LMAX) {
       const double ha = core + w[E - Lv];
       const double hb = core + w[E + 1 + Lv];
       constexpr bool shl = ROLE != 0 && pair_level_shared(E, Lv);
@@ -146,7 +185,7 @@ __device__ __forceinline__ void pair_scatter(const double (&w)[2 * E + 2], doubl
       auto tap = [&](auto dc) {
         constexpr int d = decltype(dc)::value - E;
         constexpr int s = (QA + d + P) % P;
-        if constexpr (clen(E, pair_abs(d)) == Lv) {
+        if constexpr (clen(E, pair_abs(d)) == Lv && d >= LO && d <= HI) {
           if constexpr (ROLE == 1 && pair_shared(E, d)) {
             // row B adds the pair sum
           } else if constexpr (ROLE == 2 && pair_shared(E, d + 1)) {
@@ -162,11 +201,127 @@ __device__ __forceinline__ void pair_scatter(const double (&w)[2 * E + 2], doubl
     }
   };
   static_for<E>(level);
-  acc[0][QA] = fma(kc, w[E], acc[0][QA]);
-  acc[1][QA] = fma(kc, w[E + 1], acc[1][QA]);
+  if constexpr (0 >= LO && 0 <= HI) {
+    acc[0][QA] = fma(kc, w[E], acc[0][QA]);
+    acc[1][QA] = fma(kc, w[E + 1], acc[1][QA]);
+  }
+}
+
+// OPT & 64: pair_scatter split in two, so that the nested windows of the two
+// rows of a pair are built in ONE instruction stream (two independent
+// dependency chains of core adds interleaved) before row A's taps; row B's
+// taps follow one row later.  Same adds in the same order per value as
+// pair_scatter: bitwise equal results.
+//   hv[L][c]: H_L of the lane's column c (c = 0: a, 1: b) at every used level
+template <int E, int LMAX>
+__device__ __forceinline__ void pair_levels(const double (&w)[2 * E + 2], double (&hv)[E + 1][2]) {
+  double core = w[E] + w[E + 1];
+  static_for<E>([&](auto lc) __attribute__((always_inline)) {
+    constexpr int Lv = decltype(lc)::value + 1;
+    if constexpr (Lv > 1 && Lv <= LMAX) core = core + (w[E + 1 - Lv] + w[E + Lv]);
+    if constexpr (pair_level_used(E, Lv) && Lv <= LMAX) {
+      hv[Lv][0] = core + w[E - Lv];
+      hv[Lv][1] = core + w[E + 1 + Lv];
+    }
+  });
+}
+
+template <int E, int LMA, int LMB>
+__device__ __forceinline__ void pair_levels2(const double (&wa)[2 * E + 2], const double (&wb)[2 * E + 2],
+                                             double (&ha)[E + 1][2], double (&hb)[E + 1][2]) {
+  double ca = wa[E] + wa[E + 1];
+  double cb = wb[E] + wb[E + 1];
+  static_for<E>([&](auto lc) __attribute__((always_inline)) {
+    constexpr int Lv = decltype(lc)::value + 1;
+    if constexpr (Lv > 1 && Lv <= LMA) ca = ca + (wa[E + 1 - Lv] + wa[E + Lv]);
+    if constexpr (Lv > 1 && Lv <= LMB) cb = cb + (wb[E + 1 - Lv] + wb[E + Lv]);
+    if constexpr (pair_level_used(E, Lv) && Lv <= LMA) {
+      ha[Lv][0] = ca + wa[E - Lv];
+      ha[Lv][1] = ca + wa[E + 1 + Lv];
+    }
+    if constexpr (pair_level_used(E, Lv) && Lv <= LMB) {
+      hb[Lv][0] = cb + wb[E - Lv];
+      hb[Lv][1] = cb + wb[E + 1 + Lv];
+    }
+  });
+}
+
+// the taps of pair_scatter from precomputed levels hv (this row) and hA (row
+// A's, for row B's pair sums)
+template <int E, int QA, int ROLE, int LO = -E, int HI = E>
+__device__ __forceinline__ void pair_taps(const double (&w)[2 * E + 2], const double (&hv)[E + 1][2],
+                                          const double (&hA)[E + 1][2], double (&acc)[2][pair_slots(E)],
+                                          double kc) {
+  constexpr int P = pair_slots(E);
+  constexpr int SF = (QA + E) % P;
+  constexpr int SL = (QA + P - E) % P;
+  if constexpr (E >= LO && E <= HI) {
+    acc[0][SF] = w[E];
+    acc[1][SF] = w[E + 1];
+  }
+  if constexpr (-E >= LO && -E <= HI) {
+    acc[0][SL] += w[E];
+    acc[1][SL] += w[E + 1];
+  }
+  static_for<E>([&](auto lc) __attribute__((always_inline)) {
+    constexpr int Lv = decltype(lc)::value + 1;
+    if constexpr (pair_level_used(E, Lv)) {
+      static_for<2 * E + 1>([&](auto dc) __attribute__((always_inline)) {
+        constexpr int d = decltype(dc)::value - E;
+        constexpr int s = (QA + d + P) % P;
+        if constexpr (clen(E, pair_abs(d)) == Lv && d >= LO && d <= HI) {
+          if constexpr (ROLE == 1 && pair_shared(E, d)) {
+            // row B adds the pair sum
+          } else if constexpr (ROLE == 2 && pair_shared(E, d + 1)) {
+            acc[0][s] += hA[Lv][0] + hv[Lv][0];
+            acc[1][s] += hA[Lv][1] + hv[Lv][1];
+          } else {
+            acc[0][s] += hv[Lv][0];
+            acc[1][s] += hv[Lv][1];
+          }
+        }
+      });
+    }
+  });
+  if constexpr (0 >= LO && 0 <= HI) {
+    acc[0][QA] = fma(kc, w[E], acc[0][QA]);
+    acc[1][QA] = fma(kc, w[E + 1], acc[1][QA]);
+  }
+}
+
+// tap bounds of one row of a pass (LO, HI) and of the next row (PI: the
+// pair's row B, whose levels row A builds)
+// LEAN_ (OPT & 256): a row of a period known to lie wholly inside the
+// segment's rows and the lattice, past the warm-up -- no per-row range,
+// emission or lattice-edge tests and the barrier placement a template
+// constant (B divides the period), so the period runs without branches
+template <int LO_, int HI_, int LON_, int HIN_, bool LEAN_ = false>
+struct PairRowBounds {
+  static constexpr int LO = LO_, HI = HI_, LON = LON_, HIN = HIN_;
+  static constexpr bool LEAN = LEAN_;
+};
+
+// OPT & 128: the tail rows of a segment skip their taps into output rows that
+// are never emitted, like the head (OPT & 16) -- possible where the last
+// period's slots are template constants, i.e. when the segment's u^t row
+// count n_in = seg + 4E is congruent to pair_tail_c(E) modulo the period: the
+// host's one-round segment height at 4096^2 (C2; nlh_api.cpp sizes()).  Other
+// segments take the generic loop.  Stage 1's tail is its last X1 rows, stage
+// 2's its last X2 iterations (each >= 2E, the period-aligned end).
+__host__ __device__ constexpr int pair_tail_c(int E) {
+  // (seg + 4E) mod period at the C2 segment height of each E
+  return E == 8 ? 4 : -1;
+}
+__host__ __device__ constexpr int pair_tail_len(int E, int c) {
+  const int P = pair_slots(E);
+  int x = ((c % P) + P) % P;
+  while (x < 2 * E) x += P;
+  return x;
 }
 
 // ABL: timing-decomposition masks for the tools/ harness (tools/pair_bench.hip).
+// 4096 / 8192: eight extra s_nop per row on wave 0 / wave 1 (the cost of
+// non-VALU instructions on each role's path).
 // libnlh instantiates ABL = 0 only (tests/test_capi.py checks the library's
 // kernel symbols); with ABL != 0 the results are meaningless.  k_pair_split:
 // 2 = no HBM traffic (no DMA, no stores; same instruction stream otherwise),
@@ -289,11 +444,17 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
 #pragma unroll
     for (int j = 0; j < P; ++j) acc[c][j] = 0.0;
   double hs[R][E + 1];  // row A's windows at the shared levels, until row B
+  constexpr bool PF = ((OPT & 32) != 0 || (OPT & 64) != 0) && B == 2 && (P & 1) == 0;
+  constexpr bool PI = (OPT & 64) != 0 && PF && PAIRS;  // row pairs' levels interleaved
+  double wr[2][NW];     // the row's window (and, PF, the next row's)
+  [[maybe_unused]] double hv[2][E + 1][2];  // PI: the levels of a pair's rows A, B
 
-  // barriers: one prologue barrier, then one after every iteration i with
-  // i % B == B-1, for i = 0 .. i_last (wave 0 stops computing at n_in - 1)
+  // ABL & 2048 (tools/pair_bench.hip only): per wave, HW_ID, XCC_ID and the
+  // s_memrealtime stamps at entry and exit into the uint64 buffer at Rc.lw
+  [[maybe_unused]] uint64_t t_entry = 0;
+  if constexpr ((ABL & 2048) != 0) t_entry = __builtin_amdgcn_s_memrealtime();
   if constexpr ((OPT & 8) != 0)
-    if (wave == 1) __builtin_amdgcn_s_setprio(3);
+    if (wave == ((OPT & 512) != 0 ? 0 : 1)) __builtin_amdgcn_s_setprio(3);
   if (wave == 0) {
     // ---- stage 1 on u^t row i
     const int gny = (int)C.ny;
@@ -308,17 +469,34 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
     const double qs = TEST ? C.dt / alpha : 0.0;
     row_barrier();  // prologue: rows 0 .. B-1 landed
     int bs = 0;     // b % K
-    for (int b = 0; b < n_in; b += P) {
-      auto body = [&](auto qc) {
+    // OPT & 16: the first period (rows 0 .. P-1) peeled with the head taps
+    // of pair_scatter left out (row i's outputs i+d < E are never emitted);
+    // OPT & 128: the last X1 rows likewise (outputs i+d >= n_in - E)
+    constexpr bool HEAD = (OPT & 16) != 0;
+    int b = 0;
+    auto body = [&](auto qc, auto bc) __attribute__((always_inline)) {
         constexpr int q = decltype(qc)::value;
+        using RB = decltype(bc);
+        constexpr int LO = RB::LO, HI = RB::HI;
         constexpr int so = (q + P - E) % P;  // output row i - E completes
         const int i = b + q;
-        if constexpr ((ABL & 32) == 0)
+        if constexpr ((ABL & 32) == 0 && !RB::LEAN)
           if (i >= n_in) return;
-        double w[NW];
-        window(ring + ((bs + q) & (K - 1)) * RW + R * lane, w);
-        pair_scatter<E, q, PAIRS ? 1 + (q & 1) : 0>(w, acc, kc, hs);
-        if ((ABL & 32) != 0 || i >= 2 * E) {
+        // OPT & 32 (B == 2 and an even period, so a row's place in its barrier
+        // block is a template constant): a block's first row also reads the
+        // second row's window, which the last barrier already published
+        double (&w)[NW] = wr[q & 1];
+        if constexpr (!PF || (q & 1) == 0) window(ring + ((bs + q) & (K - 1)) * RW + R * lane, w);
+        if constexpr (PF && (q & 1) == 0) window(ring + ((bs + q + 1) & (K - 1)) * RW + R * lane, wr[1]);
+        if constexpr (PI) {
+          if constexpr ((q & 1) == 0)
+            pair_levels2<E, pair_head_lmax<E, LO, HI>(), pair_head_lmax<E, RB::LON, RB::HIN>()>(wr[0], wr[1],
+                                                                                               hv[0], hv[1]);
+          pair_taps<E, q, 1 + (q & 1), LO, HI>(w, hv[q & 1], hv[0], acc, kc);
+        } else {
+          pair_scatter<E, q, PAIRS ? 1 + (q & 1) : 0, LO, HI>(w, acc, kc, hs);
+        }
+        if (RB::LEAN || (ABL & 32) != 0 || i >= 2 * E) {
           const int m = i - 2 * E;
           const int gy = gy1first + ydir * m;
           double v0 = mcol[0] * acc[0][so];
@@ -337,7 +515,12 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
             if (mcol[0] == 0.0) v0 = 0.0;  // columns outside the lattice
             if (mcol[1] == 0.0) v1 = 0.0;
           }
-          if (gy < 0 || gy >= gny) {
+          if constexpr (RB::LEAN) {
+            // lean rows: a select (v_cndmask on a wave-uniform condition), no branch
+            const bool out = gy < 0 || gy >= gny;
+            v0 = out ? 0.0 : v0;
+            v1 = out ? 0.0 : v1;
+          } else if (gy < 0 || gy >= gny) {
             v0 = 0.0;
             v1 = 0.0;
           }
@@ -348,11 +531,64 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
           if constexpr (TEST)
             *reinterpret_cast<double2 *>(qbuf + (m & (U1R - 1)) * U1W + R * lane) = make_double2(q0, q1);
         }
-        if constexpr ((ABL & 40) != 40)
-          if ((i & (B - 1)) == B - 1) row_barrier();
-      };
-      static_for<P>(body);
+        if constexpr ((ABL & 4096) != 0)
+          asm volatile("s_nop 0\n\ts_nop 0\n\ts_nop 0\n\ts_nop 0\n\ts_nop 0\n\ts_nop 0\n\ts_nop 0\n\ts_nop 0");
+        if constexpr ((ABL & 40) != 40) {
+          if constexpr (RB::LEAN) {
+            if constexpr ((q & (B - 1)) == B - 1) row_barrier();
+          } else if ((i & (B - 1)) == B - 1) {
+            row_barrier();
+          }
+        }
+        // lean rows have no branch between them: without a scheduling fence
+        // per row hipcc interleaves whole periods and spills
+        if constexpr (RB::LEAN) __builtin_amdgcn_sched_barrier(0);
+    };
+    if constexpr (HEAD) {  // n_in >= 4E+1 >= P: every row of the first period exists
+      static_for<P>([&](auto qc) __attribute__((always_inline)) {
+        constexpr int q = decltype(qc)::value;
+        body(qc, PairRowBounds<(q < 2 * E ? E - q : -E), E, (q + 1 < 2 * E ? E - q - 1 : -E), E>{});
+      });
+      bs = P & (K - 1);
+      b = P;
+    }
+    // OPT & 128: the last X1 rows in two period-aligned parts (tail_ok: this
+    // segment's n_in has the congruence pair_tail_c names)
+    constexpr int TC = (OPT & 128) != 0 ? pair_tail_c(E) : -1;
+    constexpr int X1 = TC >= 0 ? pair_tail_len(E, TC) : 0;
+    const bool tail_ok = TC >= 0 && HEAD && n_in >= P + X1 && (n_in - TC) % P == 0;
+    const int bend = tail_ok ? n_in - X1 : n_in;
+    // OPT & 256: the periods after the head that lie wholly inside the
+    // segment's rows run lean (past the warm-up: b >= P > 2E); the rest of
+    // the rows (a partial last period) take the checked body.  Sequential
+    // loops, not a lean / checked choice per period: hipcc spills when one
+    // loop holds two copies of the period
+    constexpr bool LEANOK = (OPT & 256) != 0 && HEAD && (P % B) == 0 && (ABL & 32) == 0;
+    static_assert(!LEANOK || P >= 2 * E, "lean periods start past the warm-up");
+    if constexpr (LEANOK) {
+      for (; b + P <= bend; b += P) {
+        static_for<P>([&](auto qc) __attribute__((always_inline)) {
+          body(qc, PairRowBounds<-E, E, -E, E, true>{});
+        });
+        bs = (bs + P) & (K - 1);
+      }
+    }
+    for (; b < bend; b += P) {
+      static_for<P>([&](auto qc) __attribute__((always_inline)) { body(qc, PairRowBounds<-E, E, -E, E>{}); });
       bs = (bs + P) & (K - 1);
+    }
+    if constexpr (TC >= 0) {
+      if (tail_ok) {
+        static_for<(X1 + P - 1) / P>([&](auto pc) __attribute__((always_inline)) {
+          constexpr int part = decltype(pc)::value;
+          static_for<P>([&](auto qc) __attribute__((always_inline)) {
+            constexpr int r = part * P + decltype(qc)::value;  // tail row: i = n_in - X1 + r
+            if constexpr (r < X1) body(qc, PairRowBounds<-E, X1 - 1 - r - E, -E, X1 - 2 - r - E>{});
+          });
+          b += P;
+          bs = (bs + P) & (K - 1);
+        });
+      }
     }
     // the block-end barriers of wave 1's iterations n_in .. i_last
     for (int j = (i_last + 1) / B - n_in / B; j > 0; --j) row_barrier();
@@ -430,28 +666,40 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
     // OPT & 1: output row of iteration i (row yout0 + ydir (m2 - 2E)), advanced
     // by one row per iteration; starts at i = P
     double *dstp = run + (int64_t)(yout0 + ydir * (P - 4 * E - B)) * pitch;
-    for (int b = P; b <= i_last; b += P) {
-      auto body = [&](auto qc) {
+    int b = P;
+    auto body = [&](auto qc, auto bc) __attribute__((always_inline)) {
         constexpr int q = decltype(qc)::value;
+        using RB = decltype(bc);
+        constexpr int LO2 = RB::LO, HI2 = RB::HI;
         constexpr int q2 = ((q - 2 * E - B) % P + P) % P;  // slot of row m2 = i - 2E - B (same parity as i)
         constexpr int so = (q2 + P - E) % P;
         const int i = b + q;
-        if constexpr ((ABL & 32) == 0)
+        if constexpr ((ABL & 32) == 0 && !RB::LEAN)
           if (i > i_last) return;
         issue((bs + q + DT) & (K - 1));  // u^t row i+DT (clamped; never a slot wave 0 still reads)
         // u^{t+1} row m2 = i - 2E - B (m2 mod P == q2); rows m2 < 0 are LDS
         // garbage that only reaches accumulators of rows never emitted, each
         // assigned afresh before use
         const int m2 = i - 2 * E - B;
-        double w2[NW];
-        window(u1buf + (m2 & (U1R - 1)) * U1W + R * lane, w2);
-        pair_scatter<E, q2, PAIRS ? 1 + (q2 & 1) : 0>(w2, acc, kc, hs);
+        // OPT & 32: u^{t+1} row m2+1 was written by wave 0 in the previous block
+        double (&w2)[NW] = wr[q & 1];
+        if constexpr (!PF || (q & 1) == 0) window(u1buf + (m2 & (U1R - 1)) * U1W + R * lane, w2);
+        if constexpr (PF && (q & 1) == 0) window(u1buf + ((m2 + 1) & (U1R - 1)) * U1W + R * lane, wr[1]);
+        if constexpr (PI) {
+          static_assert((q2 & 1) == (q & 1), "row pairs follow the barrier blocks");
+          if constexpr ((q & 1) == 0)
+            pair_levels2<E, pair_head_lmax<E, LO2, HI2>(), pair_head_lmax<E, RB::LON, RB::HIN>()>(
+                wr[0], wr[1], hv[0], hv[1]);
+          pair_taps<E, q2, 1 + (q2 & 1), LO2, HI2>(w2, hv[q & 1], hv[0], acc, kc);
+        } else {
+          pair_scatter<E, q2, PAIRS ? 1 + (q2 & 1) : 0, LO2, HI2>(w2, acc, kc, hs);
+        }
         if constexpr (TEST) {  // (dt/alpha) b(t+1) at the centre row of the output
           const double *qr = qbuf + (m2 & (U1R - 1)) * U1W + R * lane + E;
           acc[0][q2] += qr[0];
           acc[1][q2] += qr[1];
         }
-        if ((ABL & 32) != 0 || m2 >= 2 * E) {
+        if (RB::LEAN || (ABL & 32) != 0 || m2 >= 2 * E) {
           const double o0 = alpha * acc[0][so];
           const double o1 = alpha * acc[1][so];
           double *dst = (OPT & 1) ? dstp : run + (int64_t)(yout0 + ydir * (m2 - 2 * E)) * pitch;
@@ -475,12 +723,81 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
           }
         }
         if constexpr ((OPT & 1) != 0) dstp += stride;
-        if constexpr ((ABL & 40) != 40) block_end(i);
-      };
-      static_for<P>(body);
+        if constexpr ((ABL & 8192) != 0)
+          asm volatile("s_nop 0\n\ts_nop 0\n\ts_nop 0\n\ts_nop 0\n\ts_nop 0\n\ts_nop 0\n\ts_nop 0\n\ts_nop 0");
+        if constexpr ((ABL & 40) != 40) {
+          if constexpr (RB::LEAN && (ABL & 64) == 0) {
+            // lean: a block end is a template constant and stores have begun
+            // the stores of iterations j-D+1 .. j (D) follow row j+B's DMA
+            // at every lean block end j (b >= 2P; static_assert below)
+            if constexpr ((q & (B - 1)) == B - 1) {
+              wait_vmcnt<D * GA + D>();
+              row_barrier();
+            }
+          } else {
+            block_end(i);
+          }
+        }
+        if constexpr (RB::LEAN) __builtin_amdgcn_sched_barrier(0);
+    };
+    // head period (b == P): m2 = q + P - 2E - B, outputs m2+d < E never emitted
+    constexpr auto head_lo = [](int m) constexpr { return m < 2 * E ? (E - m > E + 1 ? E + 1 : E - m) : -E; };
+    if constexpr ((OPT & 16) != 0) {
+      static_for<P>([&](auto qc) __attribute__((always_inline)) {
+        constexpr int m2h = decltype(qc)::value + P - 2 * E - B;
+        body(qc, PairRowBounds<head_lo(m2h), E, head_lo(m2h + 1), E>{});
+      });
+      bs = (bs + P) & (K - 1);
+      b += P;
+    }
+    // OPT & 128: the last X2 iterations, outputs m2+d >= nm - E never emitted
+    constexpr int TC = (OPT & 128) != 0 ? pair_tail_c(E) : -1;
+    constexpr int X2 = TC >= 0 ? pair_tail_len(E, TC + B) : 0;
+    const bool tail_ok = TC >= 0 && (OPT & 16) != 0 && i_last + 1 - X2 >= 2 * P && (n_in - TC) % P == 0;
+    const int bend = tail_ok ? i_last + 1 - X2 : i_last + 1;
+    // OPT & 256: the periods from the first after the head (b = 2P) that lie
+    // wholly inside the iterations run lean; a partial last period the
+    // checked body (sequential loops, as stage 1)
+    constexpr bool LEANOK = (OPT & 1024) != 0 && (OPT & 16) != 0 && (P % B) == 0 && (ABL & 32) == 0;
+    // b >= 2P: every row emits (m2 = i - 2E - B >= 2E) and at every block end
+    // j the stores of iterations j-D+1 .. j have been issued (j-D+1 >= 4E+B)
+    static_assert(!LEANOK || (2 * P - 2 * E - B >= 2 * E && 2 * P + B - D >= 4 * E + B), "lean from b = 2P");
+    if constexpr (LEANOK) {
+      for (; b + P <= bend; b += P) {
+        static_for<P>([&](auto qc) __attribute__((always_inline)) {
+          body(qc, PairRowBounds<-E, E, -E, E, true>{});
+        });
+        bs = (bs + P) & (K - 1);
+      }
+    }
+    for (; b < bend; b += P) {
+      static_for<P>([&](auto qc) __attribute__((always_inline)) { body(qc, PairRowBounds<-E, E, -E, E>{}); });
       bs = (bs + P) & (K - 1);
     }
+    if constexpr (TC >= 0) {
+      if (tail_ok) {
+        static_for<(X2 + P - 1) / P>([&](auto pc) __attribute__((always_inline)) {
+          constexpr int part = decltype(pc)::value;
+          static_for<P>([&](auto qc) __attribute__((always_inline)) {
+            constexpr int r = part * P + decltype(qc)::value;  // tail iteration: i = i_last + 1 - X2 + r
+            if constexpr (r < X2) body(qc, PairRowBounds<-E, X2 - 1 - r - E, -E, X2 - 2 - r - E>{});
+          });
+          b += P;
+          bs = (bs + P) & (K - 1);
+        });
+      }
+    }
     wait_vmcnt<0>();  // drain the tail DMAs and the stores
+  }
+  if constexpr ((ABL & 2048) != 0) {
+    const uint64_t t_exit = __builtin_amdgcn_s_memrealtime();
+    if (lane == 0) {
+      uint64_t *rec = reinterpret_cast<uint64_t *>(const_cast<double *>(Rc.lw)) + 4 * (2 * blockIdx.x + wave);
+      rec[0] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID
+      rec[1] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
+      rec[2] = t_entry;
+      rec[3] = t_exit;
+    }
   }
 }
 

@@ -3,7 +3,14 @@
 
 namespace nlh {
 
-bool prefix_rt_supported(int E) { return E >= 65 && E <= 224; }
+// 65 .. 224: one staged chunk (k_prefix_rt); past 224 the chunked k_prefix_rtc
+// up to kPrefixMaxE (its LDS: 2 (64 x 8 x nchk + 2) doubles <= 41 KB)
+bool prefix_rt_supported(int E) { return E >= 65 && E <= kPrefixMaxE; }
+
+// chunks of 64 x 8 columns k_prefix_rtc stages (64 + 2E rounded up to even)
+static int prefix_rtc_chunks(int E) { return (64 + 2 * E + (E & 1) * 2 + 511) / 512; }
+
+int prefix_rt_window(int E) { return E <= 224 ? 512 : 512 * prefix_rtc_chunks(E); }
 
 int prefix_rt_table_size(int E) { return 2 * (E + kPrefixRows) + 1; }
 
@@ -38,7 +45,17 @@ int launch_prefix_rt(const RectList &rl, const StepConst &c, const void *table, 
   if (c.E <= 96) return test ? launch_nv<4, true>(rl, c, table, st) : launch_nv<4, false>(rl, c, table, st);
   if (c.E <= 160) return test ? launch_nv<6, true>(rl, c, table, st) : launch_nv<6, false>(rl, c, table, st);
   if (c.E <= 224) return test ? launch_nv<8, true>(rl, c, table, st) : launch_nv<8, false>(rl, c, table, st);
-  return -1;
+  if (c.E > kPrefixMaxE) return -1;
+  const int nchk = prefix_rtc_chunks(c.E);
+  const size_t lds = 2 * (size_t)(512 * nchk + 2) * sizeof(double);
+  if (test)
+    hipLaunchKernelGGL((k_prefix_rtc<8, kPrefixRows, true>), dim3(rl.nwork), dim3(64), lds, st, rl, c,
+                       (const int2 *)table, nchk);
+  else
+    hipLaunchKernelGGL((k_prefix_rtc<8, kPrefixRows, false>), dim3(rl.nwork), dim3(64), lds, st, rl, c,
+                       (const int2 *)table, nchk);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : (int)e;
 }
 
 }  // namespace nlh

@@ -8,8 +8,12 @@
 namespace nlh {
 
 constexpr int kPrefixRows = 32;  // R: output rows per work item (the rect lists' seg_rows)
-// horizons k_prefix_rt serves: 65 .. 224 (staged window 64 + 2E <= 512 columns)
+// horizons k_prefix_rt serves: 65 .. 224 (staged window 64 + 2E <= 512
+// columns), k_prefix_rtc past that (the window in 512-column chunks)
+constexpr int kPrefixMaxE = 992;
 bool prefix_rt_supported(int E);
+// columns staged from x0 - E of a strip (the block's right padding covers them)
+int prefix_rt_window(int E);
 // host table of 2 (E + R) + 1 int2 entries, index d + E + R: {L, -L - 1}
 // with L = len(|d|) for |d| <= E, {0, 0} beyond
 int prefix_rt_table_size(int E);

@@ -70,14 +70,18 @@ def check_l2(l2, l2_ref, u, u_ref, what: str = "") -> float:
     + sum d^2 (Cauchy-Schwarz).  The regime follows that bound:
     * 1e-10 relative, where the bound itself is below 1e-10 of l2_ref -- the
       per-node agreement leaves no room for more, so the L2 must match to that;
-    * 1e-10 absolute, where a few-ulp per-node difference can already move the
-      L2 by more than 1e-10 relative (the reference's own error is then at the
-      rounding floor of the field: C4's 100 steps, 3.6e-10 rms per node, give
-      6.5e-6 relative from 1.2e-15 rms differences; k_prefix_rt's eps 65-130
-      runs 1.1-4.8e-10 relative from <= 1.5e-13 per node);
+    * the bound itself, where it exceeds 1e-10 of l2_ref: a few-ulp per-node
+      difference can then move the L2 by more than 1e-10 relative (the
+      reference's own error is at the rounding floor of the field: C4's 100
+      steps, 3.6e-10 rms per node, give 6.5e-6 relative from 1.2e-15 rms
+      differences; k_prefix_rt's eps 65-130 runs 1.1-4.8e-10 relative from
+      <= 1.5e-13 per node).  This is AUTO's test-mode L2 contract there
+      (include/nlh.h): 1e-10 relative only where the
+      reference's error is above the rounding floor of the node differences;
     * always: the L2 difference is the one the measured d imply (within the
-      bound above, up to the reductions' own rounding) -- the norm kernel adds
-      nothing of its own.
+      bound above plus 1e-13 of l2_ref for the two reductions' own rounding)
+      -- the norm kernel adds nothing of its own.  (Round 4 asserted a fixed
+      1e-10 absolute in the second regime, vacuous for l2_ref < 1e-10.)
     The observed relative difference, the bound and the regime go to
     gpurun_out/parity_l2.jsonl.  Returns the relative difference."""
     import json
@@ -93,13 +97,69 @@ def check_l2(l2, l2_ref, u, u_ref, what: str = "") -> float:
     rec = {"test": os.environ.get("PYTEST_CURRENT_TEST", "").split(" ")[0], "what": what, "n": n,
            "l2": l2, "l2_ref": l2_ref, "rel_diff": rel, "abs_diff": diff, "cauchy_schwarz_bound": cs,
            "error_per_node_rms": float(np.sqrt(l2_ref / n)), "field_scale": scale,
-           "criterion": "1e-10 relative" if relative else "1e-10 absolute (rounding floor: bound > 1e-10 relative)",
+           "criterion": "1e-10 relative" if relative else "Cauchy-Schwarz bound (rounding floor: bound > 1e-10 relative)",
            "max_node_diff": float(np.max(np.abs(u - u_ref)))}
     try:
         with open(os.path.join(_record_dir(), "parity_l2.jsonl"), "a") as f:
             f.write(json.dumps(rec) + "\n")
     except OSError:
         pass
-    assert diff <= (1e-10 * l2_ref if relative else 1e-10), rec
-    assert diff <= cs * (1 + 1e-9) + 1e-13 * l2_ref + 1e-300, rec
+    if relative:
+        assert diff <= 1e-10 * l2_ref, rec
+    assert diff <= cs * (1 + 1e-9) + 1e-13 * l2_ref, rec
     return rel
+
+
+def node_errors(u, u_ref, scale=None, rows=2048) -> dict:
+    """Per-node error statistics of u against u_ref, chunked over rows so
+    full-size fields need no full-size temporaries: the max absolute
+    difference, the field scale (max |u_ref| unless given), and north_star's
+    per-node RELATIVE error |u - u_ref| / |u_ref| -- its maximum over the nodes
+    with |u_ref| >= 1e-6 and >= 1e-3 of the scale (near the field's zero
+    crossings a relative error says nothing: a node's rounding follows the
+    magnitude of the neighbours it sums, not its own) and the fraction of
+    those nodes within 1e-12 relative."""
+    import numpy as np
+    a = np.asarray(u, dtype=np.float64)
+    b = np.asarray(u_ref, dtype=np.float64)
+    a2 = a.reshape(a.shape[0], -1) if a.ndim > 1 else a.reshape(1, -1)
+    b2 = b.reshape(b.shape[0], -1) if b.ndim > 1 else b.reshape(1, -1)
+    sc = float(np.max(np.abs(b))) if scale is None else float(scale)
+    dmax = 0.0
+    rel6 = rel3 = 0.0
+    n6 = ok6 = 0
+    for y in range(0, a2.shape[0], rows):
+        x = a2[y:y + rows]
+        r = b2[y:y + rows]
+        d = np.abs(x - r)
+        dmax = max(dmax, float(np.max(d)) if d.size else 0.0)
+        ar = np.abs(r)
+        m6 = ar >= 1e-6 * sc
+        if np.any(m6):
+            q = d[m6] / ar[m6]
+            rel6 = max(rel6, float(np.max(q)))
+            n6 += int(q.size)
+            ok6 += int(np.count_nonzero(q <= 1e-12))
+        m3 = ar >= 1e-3 * sc
+        if np.any(m3):
+            rel3 = max(rel3, float(np.max(d[m3] / ar[m3])))
+    return {"max_abs_diff": dmax, "field_scale": sc, "max_rel_node_1e-6": rel6, "max_rel_node_1e-3": rel3,
+            "nodes_1e-6": n6, "frac_nodes_rel_le_1e-12": (ok6 / n6) if n6 else 1.0}
+
+
+def check_nodes(u, u_ref, what: str = "", scale=None, tol: float = 1e-12) -> dict:
+    """The per-node criterion of every FAST kernel: |u - u_ref|
+    <= tol * field scale at every node, asserted; north_star's per-node
+    relative error (node_errors) recorded beside it, before the assertion, to
+    gpurun_out/parity_nodes.jsonl."""
+    import json
+    st = node_errors(u, u_ref, scale)
+    rec = {"test": os.environ.get("PYTEST_CURRENT_TEST", "").split(" ")[0], "what": what,
+           "n": int(getattr(u_ref, "size", 0)), "tol_field_scale": tol, **st}
+    try:
+        with open(os.path.join(_record_dir(), "parity_nodes.jsonl"), "a") as f:
+            f.write(json.dumps(rec) + "\n")
+    except OSError:
+        pass
+    assert st["max_abs_diff"] <= tol * st["field_scale"], rec
+    return st

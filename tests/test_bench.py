@@ -29,7 +29,7 @@ def test_spawned_ranks_fail_loudly_without_gpu():
                        timeout=240, cwd=ROOT)
     assert p.returncode != 0
     assert "no HIP device" in p.stderr, p.stderr[-2000:]
-    assert '"metric"' not in p.stdout
+    assert '"value"' not in p.stdout  # no result line: only the error line (round 5)
 
 
 def test_world_size_mismatch_is_an_error():
@@ -75,3 +75,70 @@ def test_cpu_baseline_bounded_sample():
     assert big["serial_1core"]["cores"] == 1 and big["serial_1core"]["value"] > 0
     small = bench.cpu_baseline(2, 256, 2, budget_s=2.0, serial_budget_s=0.05)
     assert small["value"] > 0 and "step(s)" in small["sample"]
+
+
+def _bench(args, env_extra=None, timeout=240):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env, capture_output=True,
+                          text=True, timeout=timeout, cwd=ROOT)
+
+
+def _error_line(stdout):
+    import json
+    lines = [l for l in stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, stdout
+    rec = json.loads(lines[0])
+    assert "metric" in rec and "value" not in rec
+    return rec
+
+
+def test_error_line_single_rank_nlh_create():
+    """a rank that fails prints ONE JSON line with the error,
+    its rank and the stage (here nlh_create: no HIP device on this machine)
+    and exits non-zero."""
+    p = _bench(["--gpus", "1", "--steps", "1", "--warmup", "0", "--no-cpu-baseline", "--pmc", "off"])
+    assert p.returncode != 0
+    rec = _error_line(p.stdout)
+    assert rec["stage"] == "nlh_create" and rec["rank"] == 0 and "no HIP device" in rec["error"], rec
+
+
+def test_error_line_spawned_ranks():
+    """--gpus 2 without WORLD_SIZE: the launcher prints the error line of the
+    first rank that failed (and nothing else on stdout)."""
+    p = _bench(["--gpus", "2", "--steps", "1", "--warmup", "0", "--no-cpu-baseline"])
+    assert p.returncode != 0
+    rec = _error_line(p.stdout)
+    # without a GPU the first device call is rank 0's RCCL id (stage comm_id);
+    # the other rank then waits in the id broadcast and is stopped
+    assert rec["stage"] in ("comm_id", "nlh_create") and rec["rank"] in (0, 1) and rec["n_gpus"] == 2, rec
+    assert "no HIP device" in rec["error"], rec
+
+
+def test_error_line_on_hang_torchrun_form():
+    """A rank that hangs in a stage (test hook NLH_BENCH_HANG_STAGE; a real
+    hang would be the RCCL rendezvous or a collective) is ended by the stage
+    watchdog: one error line naming the stage, exit 124.  WORLD_SIZE set, as
+    torch.distributed.run launches it."""
+    import json
+    env = {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0", "MASTER_ADDR": "127.0.0.1",
+           "MASTER_PORT": str(bench.free_port()), "NLH_BENCH_STAGE_TIMEOUT": "3",
+           "NLH_BENCH_HANG_STAGE": "process_group"}
+    p = _bench(["--gpus", "2", "--steps", "1", "--warmup", "0", "--no-cpu-baseline"], env, timeout=120)
+    assert p.returncode == 124, (p.returncode, p.stderr[-2000:])
+    rec = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    assert rec["stage"] == "process_group" and rec["rank"] == 0 and "did not finish" in rec["error"], rec
+
+
+def test_error_line_rendezvous_timeout():
+    """Rank 1 of 2 alone (its peer never starts): the gloo rendezvous blocks and
+    the process-group watchdog ends it with the error line."""
+    import json
+    env = {"WORLD_SIZE": "2", "RANK": "1", "LOCAL_RANK": "1", "MASTER_ADDR": "127.0.0.1",
+           "MASTER_PORT": str(bench.free_port()), "NLH_BENCH_STAGE_TIMEOUT": "5"}
+    p = _bench(["--gpus", "2", "--steps", "1", "--warmup", "0", "--no-cpu-baseline"], env, timeout=120)
+    assert p.returncode != 0
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert lines, p.stderr[-2000:]
+    rec = json.loads(lines[-1])
+    assert rec["rank"] == 1 and rec["stage"] == "process_group", rec

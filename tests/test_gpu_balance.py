@@ -15,7 +15,7 @@ import subprocess
 import numpy as np
 import pytest
 
-from conftest import ROOT, read_input
+from conftest import check_nodes, ROOT, read_input
 
 import nonlocalheatequation_amd as N
 
@@ -38,7 +38,7 @@ def _check(oracle, u, p, t, kernel, u0=None):
     if kernel == "exact":
         assert np.array_equal(u, ref)
     else:
-        assert np.max(np.abs(u - ref)) <= 1e-12 * np.max(np.abs(ref))
+        check_nodes(u, ref)
 
 
 @pytest.mark.parametrize("kernel,test,n1,n2", [("exact", True, 4, 3), ("fast", True, 3, 4),
@@ -175,7 +175,7 @@ def test_virtual_busy_measured_per_rank(monkeypatch):
         r.test_init()
         r.run(t)
         ref = r.field()
-    assert np.max(np.abs(u - ref)) <= 1e-12 * np.max(np.abs(ref))
+    check_nodes(u, ref)
 
 
 @pytest.mark.parametrize("target", [
@@ -217,9 +217,9 @@ def test_repartition_large_messages(monkeypatch, target):
         r.run(6)
         ref = r.field()
     scale = np.max(np.abs(ref))
-    assert np.max(np.abs(g - ref4)) <= 1e-12 * scale
+    check_nodes(g, ref4, scale=scale)
     del g, ref4
-    assert np.max(np.abs(u - ref)) <= 1e-12 * scale
+    check_nodes(u, ref, scale=scale)
 
 
 def test_busy_time_within_wall_time():

@@ -7,10 +7,16 @@ size-independent properties, where the CPU oracle would take minutes.
 * linearity of the explicit step (test=0): step(2u) == 2 step(u) bit for bit
   (scaling by 2 is exact through every add, multiply and fma);
 * mirror symmetry of the J=1 disk operator: stepping the x-reflected field
-  gives the reflected result (rounding only, the sweep order differs).
+  gives the reflected result (rounding only, the sweep order differs);
+* C2 at its stated run length (BASELINE.json configs[1]: 1000 steps), round
+  5: the production pass and the test-mode pass (manufactured source, L2)
+  against k_exact over all 1000 steps, per node (check_nodes: 1e-12 of field
+  scale asserted, per-node relative error recorded) and by the L2 criterion.
 """
 import numpy as np
 import pytest
+
+from conftest import check_l2, check_nodes
 
 import nonlocalheatequation_amd as N
 
@@ -42,7 +48,7 @@ def test_c2_two_step_kernel_vs_parity_kernel(u0):
     ue, info_e = _step(u0, "exact", 4)
     assert info_e.kernel == N.KERNEL_EXACT
     scale = np.max(np.abs(ue))
-    assert np.max(np.abs(uf - ue)) <= 1e-12 * scale
+    check_nodes(uf, ue, scale=scale)
 
 
 @pytest.mark.parametrize("kernel", ["fast", "exact"])
@@ -56,3 +62,35 @@ def test_c2_mirror_symmetry(u0):
     a, _ = _step(u0, "fast", 2)
     b, _ = _step(np.ascontiguousarray(u0[:, ::-1]), "fast", 2)
     assert np.max(np.abs(a[:, ::-1] - b)) <= 1e-13 * np.max(np.abs(a))
+
+
+NT_C2 = 1000  # BASELINE.json configs[1]: "4096x4096 grid, eps=8 cells, 1000 steps"
+
+
+def test_c2_full_run_length_production(u0):
+    """1000 production steps (500 two-step passes) against 1000 steps of the
+    bit-parity kernel (~1.5 s at 11 G node-updates/s)."""
+    uf, info = _step(u0, "fast", NT_C2)
+    assert info.steps_per_pass == 2 and info.pass_kernel.startswith("k_pair")
+    ue, info_e = _step(u0, "exact", NT_C2)
+    assert info_e.kernel == N.KERNEL_EXACT
+    check_nodes(uf, ue, "C2 1000 steps production: k_pair_split vs k_exact")
+
+
+def test_c2_full_run_length_test_mode():
+    """1000 test-mode steps from the manufactured solution's initial field:
+    per node and the reference's L2 (error_l2 at t = 1000) against k_exact."""
+    dh = 1.0 / NX
+    dt = EPS ** 4 * dh * dh / (8 * N.disk_count(EPS))
+    out = {}
+    for kernel in ("fast", "exact"):
+        with N.Solver(NX, NX, EPS, 1.0, dt, dh, test=True, kernel=kernel) as s:
+            s.test_init()
+            s.run(NT_C2)
+            s.synchronize()
+            out[kernel] = (s.field(), s.errors(NT_C2)[0], s.info())
+    uf, l2f, info = out["fast"]
+    ue, l2e, info_e = out["exact"]
+    assert info.steps_per_pass == 2 and info_e.kernel == N.KERNEL_EXACT
+    check_nodes(uf, ue, "C2 1000 steps test mode: k_pair_split<TEST> vs k_exact")
+    check_l2(l2f, l2e, uf, ue, "C2 1000 steps test mode: k_pair_split<TEST> vs k_exact")

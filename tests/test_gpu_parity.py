@@ -10,7 +10,7 @@ error to 1e-10"):
 import numpy as np
 import pytest
 
-from conftest import check_l2, read_input
+from conftest import check_nodes, check_l2, read_input
 
 import nonlocalheatequation_amd as N
 
@@ -63,9 +63,7 @@ def test_fast_production_serial_rows(oracle, row):
     u_ref, _, _ = _oracle_run(oracle, r, False)
     u, _, _, info = _gpu_run(r, False, "fast")
     assert info.kernel == N.KERNEL_FAST
-    scale = np.max(np.abs(u_ref))
-    err = np.max(np.abs(u - u_ref))
-    assert err <= 1e-12 * scale, f"max |diff| {err} vs scale {scale}"
+    check_nodes(u, u_ref, f"tests/2d.txt row {row}, fast production")
 
 
 @pytest.mark.parametrize("row", range(len(SERIAL_ROWS)))
@@ -74,7 +72,7 @@ def test_fast_test_mode_l2(oracle, row):
     u_ref, l2_ref, li_ref = _oracle_run(oracle, r, True)
     u, l2, li, _ = _gpu_run(r, True, "fast")
     scale = np.max(np.abs(u_ref))
-    assert np.max(np.abs(u - u_ref)) <= 1e-12 * scale
+    check_nodes(u, u_ref, scale=scale)
     check_l2(l2, l2_ref, u, u_ref, f"tests/2d.txt row {row}, fast")
     assert abs(li - li_ref) <= 1e-9 * li_ref
 
@@ -93,7 +91,7 @@ def test_tiled_rows_single_gpu(oracle, row):
     assert l2 / (r.nx * r.ny) <= 1e-6
     u, l2, li, info = _gpu_run(r, True, "auto")
     assert info.kernel == N.KERNEL_FAST
-    assert np.max(np.abs(u - u_ref)) <= 1e-12 * np.max(np.abs(u_ref))
+    check_nodes(u, u_ref)
     check_l2(l2, l2_ref, u, u_ref, f"tests/2d_async.txt row {row}, auto")
 
 
@@ -111,7 +109,7 @@ def test_fast_random_ic_all_eps(oracle, eps):
     u_ref, _, _ = _oracle_run(oracle, r, False, u0)
     u, _, _, _ = _gpu_run(r, False, "fast", u0)
     scale = np.max(np.abs(u_ref))
-    assert np.max(np.abs(u - u_ref)) <= 1e-12 * scale
+    check_nodes(u, u_ref, scale=scale)
     ue, _, _, _ = _gpu_run(r, False, "exact", u0)
     assert np.array_equal(ue, u_ref)
 
@@ -135,7 +133,7 @@ def test_eps32_golden(kernel, test):
     if kernel == "exact":
         assert np.array_equal(u, g)
     else:
-        assert np.max(np.abs(u - g)) <= 1e-12 * np.max(np.abs(g))
+        check_nodes(u, g)
 
 
 @pytest.mark.parametrize("eps", [49, 52, 53, 57, 64])
@@ -154,9 +152,7 @@ def test_large_eps_64(oracle, eps, test):
     ref = oracle.run(p, nt, u0)
     u, (l2, _), info = _gpu_run_j(r, test, "auto", "constant", u0)
     assert info.pass_kernel == "k_wide" and info.kernel == N.KERNEL_FAST
-    d = np.max(np.abs(u - ref))
-    scale = np.max(np.abs(ref))
-    assert d <= 1e-12 * scale, d
+    check_nodes(u, ref, f"k_wide eps {eps}")
     if test:
         check_l2(l2, oracle.errors(p, nt, ref)[0], u, ref, f"k_wide eps {eps}")
     ue, _, info = _gpu_run_j(r, test, "exact", "constant", u0)
@@ -189,7 +185,7 @@ def test_large_eps_64_blocks(oracle, monkeypatch, eps, tiles):
         s.synchronize()
         u = s.field()
         assert s.info().pass_kernel == "k_wide"
-    assert np.max(np.abs(u - ref)) <= 1e-12 * np.max(np.abs(ref))
+    check_nodes(u, ref)
 
 
 def _smooth_noisy_ic(nx, ny, dh, seed):
@@ -223,19 +219,21 @@ def test_prefix_rt_vs_oracle(oracle, eps, test):
     ref = oracle.run(p, nt, u0)
     u, (l2, _), info = _gpu_run_j(r, test, "auto", "constant", u0)
     assert info.pass_kernel == "k_prefix_rt" and info.kernel == N.KERNEL_FAST
-    assert np.max(np.abs(u - ref)) <= 1e-12 * np.max(np.abs(ref))
+    check_nodes(u, ref)
     if test:
         check_l2(l2, oracle.errors(p, nt, ref)[0], u, ref, f"k_prefix_rt eps {eps}")
     ue, _, info = _gpu_run_j(r, test, "exact", "constant", u0)
     assert info.kernel == N.KERNEL_EXACT and np.array_equal(ue, ref)
 
 
-@pytest.mark.parametrize("tiles", [(3, 2), (1, 4)])
-def test_prefix_rt_blocks(oracle, monkeypatch, tiles):
-    """k_prefix_rt at eps 80 through the multi-block exchange (RCCL to self),
-    blocks narrower / shorter than the horizon's window, vs the oracle."""
+@pytest.mark.parametrize("tiles,eps", [((3, 2), 80), ((1, 4), 80), ((3, 2), 71), ((3, 2), 97)])
+def test_prefix_rt_blocks(oracle, monkeypatch, tiles, eps):
+    """k_prefix_rt through the multi-block exchange (RCCL to self), blocks
+    narrower / shorter than the horizon's window, vs the oracle.  Odd eps
+    (71, 97): a block with a left neighbour starts its interior at
+    x0 = eps, so every strip's 16-byte window loads are only 8-byte aligned."""
     monkeypatch.setenv("NLH_RCCL_SELF", "1")
-    nx, ny, nt, eps = 240, 200, 3, 80
+    nx, ny, nt = 240, 200, 3
     dh = 1.0 / nx
     dt = 0.7 * eps ** 4 * dh * dh / (8 * N.disk_count(eps))
     u0 = _smooth_noisy_ic(nx, ny, dh, 7)
@@ -246,13 +244,53 @@ def test_prefix_rt_blocks(oracle, monkeypatch, tiles):
         s.synchronize()
         u = s.field()
         assert s.info().pass_kernel == "k_prefix_rt" and s.info().nblocks == tiles[0] * tiles[1]
-    assert np.max(np.abs(u - ref)) <= 1e-12 * np.max(np.abs(ref))
+    check_nodes(u, ref)
 
 
-@pytest.mark.parametrize("eps", [225, 240])
+@pytest.mark.parametrize("eps", [230, 300])
+@pytest.mark.parametrize("test", [False, True])
+def test_prefix_rtc_vs_oracle(oracle, eps, test):
+    """Past 224 (staged window 64 + 2 eps > 512 columns) AUTO/FAST run the
+    chunked k_prefix_rtc (round 5; VERDICT r4: no horizon falls back to
+    k_exact): the window staged in 512-column chunks with a running total.
+    Per node within 1e-12 of field scale, L2 by the recorded criterion, vs
+    the oracle; the horizon covers the whole (small) lattice.  Oracle ~4-7 s
+    per case."""
+    nx, ny, nt = 120, 110, 2
+    dh = 1.0 / nx
+    r = N.BatchRow(nx, ny, nt, eps, 1.0, 0.05 * eps ** 4 * dh * dh / (8 * N.disk_count(eps)), dh)
+    u0 = None if test else _smooth_noisy_ic(nx, ny, dh, eps)
+    p = oracle.params(nx, ny, eps, r.k, r.dt, dh, int(test))
+    ref = oracle.run(p, nt, u0)
+    u, (l2, _), info = _gpu_run_j(r, test, "auto", "constant", u0)
+    assert info.pass_kernel == "k_prefix_rt" and info.kernel == N.KERNEL_FAST
+    check_nodes(u, ref, f"k_prefix_rtc eps {eps}")
+    if test:
+        check_l2(l2, oracle.errors(p, nt, ref)[0], u, ref, f"k_prefix_rtc eps {eps}")
+
+
+def test_prefix_rtc_blocks(oracle, monkeypatch):
+    """k_prefix_rtc at odd eps 231 through 3 x 2 blocks (RCCL to self):
+    blocks much narrower than the horizon, 8-byte-aligned window loads."""
+    monkeypatch.setenv("NLH_RCCL_SELF", "1")
+    nx, ny, nt, eps = 150, 120, 2, 231
+    dh = 1.0 / nx
+    dt = 0.05 * eps ** 4 * dh * dh / (8 * N.disk_count(eps))
+    u0 = _smooth_noisy_ic(nx, ny, dh, 11)
+    ref = oracle.run(oracle.params(nx, ny, eps, 1.0, dt, dh, 0), nt, u0)
+    with N.Solver(nx, ny, eps, 1.0, dt, dh, kernel="fast", tiles=(3, 2), split_tiles=True) as s:
+        s.input_init(u0)
+        s.run(nt)
+        s.synchronize()
+        u = s.field()
+        assert s.info().pass_kernel == "k_prefix_rt" and s.info().nblocks == 6
+    check_nodes(u, ref, "k_prefix_rtc eps 231, 3x2 blocks")
+
+
+@pytest.mark.parametrize("eps", [993, 1100])
 def test_unsupported_fast_eps_falls_back_to_exact(oracle, eps):
-    """Past k_prefix_rt's staged window (64 + 2 eps > 512 columns) AUTO runs
-    the exact kernel and an explicit FAST request is refused."""
+    """Past k_prefix_rtc's range (eps > 992: its LDS) AUTO runs the exact
+    kernel and an explicit FAST request is refused."""
     r = N.BatchRow(60, 50, 2, eps, 1.0, 1e-4, 1.0 / 60)
     with N.Solver(r.nx, r.ny, eps, r.k, r.dt, r.dh, test=False, kernel="auto") as s:
         assert s.info().kernel == N.KERNEL_EXACT
@@ -287,7 +325,7 @@ def test_wide_kernel_vs_oracle(oracle, eps, test):
     u, l2, _, info = _gpu_run(r, test, "auto", u0)
     assert info.pass_kernel == "k_wide" and info.kernel == N.KERNEL_FAST
     scale = np.max(np.abs(u_ref))
-    assert np.max(np.abs(u - u_ref)) <= 1e-12 * scale
+    check_nodes(u, u_ref, scale=scale)
     if test:
         check_l2(l2, l2_ref, u, u_ref, f"k_wide eps {eps}")
 
@@ -307,9 +345,7 @@ def test_wide_kernel_large_eps(oracle, eps, test):
     ref = oracle.run(p, nt, u0)
     u, (l2, _), info = _gpu_run_j(r, test, "auto", "constant", u0)
     assert info.pass_kernel == "k_wide" and info.kernel == N.KERNEL_FAST
-    d = np.max(np.abs(u - ref))
-    scale = np.max(np.abs(ref))
-    assert d <= 1e-12 * scale, d
+    check_nodes(u, ref, f"k_wide eps {eps}")
     if test:
         check_l2(l2, oracle.errors(p, nt, ref)[0], u, ref, f"k_wide eps {eps}")
 
@@ -329,7 +365,7 @@ def test_wide_kernel_segment_heights(oracle, seg):
         s.synchronize()
         u = s.field()
         assert s.info().pass_kernel == "k_wide"
-    assert np.max(np.abs(u - ref)) <= 1e-12 * np.max(np.abs(ref))
+    check_nodes(u, ref)
 
 
 @pytest.mark.parametrize("r", [1, 2, 4])
@@ -348,7 +384,7 @@ def test_fast_strip_width_variants(oracle, monkeypatch, r, eps):
             u_ref, l2_ref, _ = _oracle_run(oracle, r_, True, u0)
         u, l2, _, info = _gpu_run(r_, test, "fast", u0)
         assert info.kernel == N.KERNEL_FAST
-        assert np.max(np.abs(u - u_ref)) <= 1e-12 * np.max(np.abs(u_ref))
+        check_nodes(u, u_ref)
 
 
 @pytest.mark.parametrize("eps", [1, 2, 5, 8, 11, 13, 16])
@@ -366,11 +402,11 @@ def test_pair_pass_matches_oracle(oracle, monkeypatch, eps, nt):
     scale = np.max(np.abs(u_ref))
     u, _, _, info = _gpu_run(r, False, "fast", u0)
     assert info.steps_per_pass == 2 and info.halo_width == 2 * eps
-    assert np.max(np.abs(u - u_ref)) <= 1e-12 * scale
+    check_nodes(u, u_ref, scale=scale)
     monkeypatch.setenv("NLH_PAIR", "0")
     u1, _, _, info1 = _gpu_run(r, False, "fast", u0)
     assert info1.steps_per_pass == 1 and info1.halo_width == eps
-    assert np.max(np.abs(u1 - u_ref)) <= 1e-12 * scale
+    check_nodes(u1, u_ref, scale=scale)
 
 
 @pytest.mark.parametrize("eps", [1, 3, 5, 8, 12, 13, 16])
@@ -387,17 +423,17 @@ def test_pair_test_mode_matches_oracle(oracle, monkeypatch, eps, nt):
     scale = np.max(np.abs(u_ref))
     u, l2, li, info = _gpu_run(r, True, "auto")
     assert info.steps_per_pass == 2 and info.pass_kernel == "k_pair_split"
-    assert np.max(np.abs(u - u_ref)) <= 1e-12 * scale
+    check_nodes(u, u_ref, scale=scale)
     d = np.max(np.abs(u - u_ref))
     check_l2(l2, l2_ref, u, u_ref, f"k_pair_split test mode eps {eps} nt {nt}")
     assert abs(li - li_ref) <= 1e-9 * li_ref + d
     monkeypatch.setenv("NLH_PAIR_TEST", "0")  # the production-sized rings (D=8, B=4)
     u4, _, _, _ = _gpu_run(r, True, "auto")
-    assert np.max(np.abs(u4 - u_ref)) <= 1e-12 * scale
+    check_nodes(u4, u_ref, scale=scale)
     monkeypatch.setenv("NLH_PAIR", "0")
     u1, _, _, info1 = _gpu_run(r, True, "auto")
     assert info1.steps_per_pass == 1
-    assert np.max(np.abs(u1 - u)) <= 1e-12 * scale
+    check_nodes(u1, u, scale=scale)
 
 
 def test_pair_test_mode_multiblock(oracle, monkeypatch):
@@ -416,8 +452,7 @@ def test_pair_test_mode_multiblock(oracle, monkeypatch):
         l2, _ = s.errors(nt)
         info = s.info()
     assert info.nblocks == 6 and info.steps_per_pass == 2
-    d = np.max(np.abs(u - u_ref))
-    assert d <= 1e-12 * np.max(np.abs(u_ref))
+    check_nodes(u, u_ref, "k_pair_split test mode 3x2 blocks")
     check_l2(l2, l2_ref, u, u_ref, "k_pair_split test mode 3x2 blocks")
 
 
@@ -436,7 +471,7 @@ def test_pair_segment_heights(oracle, seg):
         s.synchronize()
         u = s.field()
         assert s.info().steps_per_pass == 2
-    assert np.max(np.abs(u - u_ref)) <= 1e-12 * np.max(np.abs(u_ref))
+    check_nodes(u, u_ref)
 
 
 @pytest.mark.parametrize("eps", [3, 8, 12, 16])
@@ -520,9 +555,7 @@ def test_linear_influence_weighted_fast(oracle, eps, test):
     u_ref, l2_ref, _ = _oracle_run_j(oracle, r, test, 1, u0)
     u, (l2, _), info = _gpu_run_j(r, test, "auto", "linear", u0)
     assert info.pass_kernel == "k_weighted" and info.kernel == N.KERNEL_FAST
-    d = np.max(np.abs(u - u_ref))
-    scale = np.max(np.abs(u_ref))
-    assert d <= 1e-12 * scale, (d, scale)
+    check_nodes(u, u_ref, f"k_weighted J = 1 - r eps {eps}")
     if test:
         check_l2(l2, l2_ref, u, u_ref, f"k_weighted J = 1 - r eps {eps}")
 
@@ -543,7 +576,7 @@ def test_linear_influence_multiblock_rccl_self(oracle, monkeypatch):
     assert np.array_equal(ue, u_ref)
     uf, _, info = _gpu_run_j(r, False, "fast", "linear", u0, tiles=(3, 2), split_tiles=True)
     assert info.pass_kernel == "k_weighted"
-    assert np.max(np.abs(uf - u_ref)) <= 1e-12 * np.max(np.abs(u_ref))
+    check_nodes(uf, u_ref)
 
 
 def test_linear_influence_large_eps_uses_exact():
@@ -586,4 +619,4 @@ def test_env_knobs_keep_results(oracle, monkeypatch, var, val, kernel, test):
     if kernel == "exact":
         assert np.array_equal(u, ref)
     else:
-        assert np.max(np.abs(u - ref)) <= 1e-12 * np.max(np.abs(ref))
+        check_nodes(u, ref)

@@ -13,6 +13,8 @@
 #include <cstring>
 #include <string>
 #include <vector>
+#include <algorithm>
+#include <utility>
 
 #include "nlh_pair.h"
 
@@ -84,7 +86,130 @@ int main(int argc, char **argv) {
   // only (no LDS reads, no vmcnt waits, no stores, no DMA)
   // OPT (nlh_pair.h): 1 incremental output row pointer, 2 unclamped row DMA,
   // 4 uniform single-column store, 8 wave 1 at wave priority 3
-#if defined(PB_SET_PRIO)
+#if defined(PB_SET_TRACE)
+  // -DPB_SET_TRACE: one launch of each variant with ABL 2048 (per-wave HW_ID,
+  // XCC_ID and s_memrealtime entry / exit stamps); summary on stdout, raw
+  // records to PB_TRACE_OUT (default pair_trace_<variant>.csv)
+  std::vector<Variant> vs = {
+      {"opt15", k_pair_split<E, 4, 2048, 2, false, 15>, 128, 4, 128 - 2 * E},
+      {"opt31", k_pair_split<E, 4, 2048, 2, false, 31>, 128, 4, 128 - 2 * E},
+      {"opt7", k_pair_split<E, 4, 2048, 2, false, 7>, 128, 4, 128 - 2 * E},
+      {"opt63", k_pair_split<E, 4, 2048, 2, false, 63>, 128, 4, 128 - 2 * E},
+      {"opt223", k_pair_split<E, 4, 2048, 2, false, 223>, 128, 4, 128 - 2 * E},
+      {"opt223_D8", k_pair_split<E, 8, 2048, 2, false, 223>, 128, 4, 128 - 2 * E},
+  };
+#elif defined(PB_SET_HEAD)
+  // -DPB_SET_HEAD: OPT 15 (round-4 library) against 31 (head taps left out), interleaved
+  std::vector<Variant> vs = {
+      {"opt15", k_pair_split<E, 4, 0, 2, false, 15>, 128, 4, 128 - 2 * E},
+      {"opt31", k_pair_split<E, 4, 0, 2, false, 31>, 128, 4, 128 - 2 * E},
+      {"opt15_b", k_pair_split<E, 4, 0, 2, false, 15>, 128, 4, 128 - 2 * E},
+      {"opt31_b", k_pair_split<E, 4, 0, 2, false, 31>, 128, 4, 128 - 2 * E},
+      {"opt15_c", k_pair_split<E, 4, 0, 2, false, 15>, 128, 4, 128 - 2 * E},
+      {"opt31_c", k_pair_split<E, 4, 0, 2, false, 31>, 128, 4, 128 - 2 * E},
+  };
+#elif defined(PB_SET_PF)
+  // -DPB_SET_PF: OPT 15 against 47 (within-block window prefetch), 63 (+ head skip)
+  std::vector<Variant> vs = {
+      {"opt15", k_pair_split<E, 4, 0, 2, false, 15>, 128, 4, 128 - 2 * E},
+      {"opt47", k_pair_split<E, 4, 0, 2, false, 47>, 128, 4, 128 - 2 * E},
+      {"opt63", k_pair_split<E, 4, 0, 2, false, 63>, 128, 4, 128 - 2 * E},
+      {"opt15_b", k_pair_split<E, 4, 0, 2, false, 15>, 128, 4, 128 - 2 * E},
+      {"opt47_b", k_pair_split<E, 4, 0, 2, false, 47>, 128, 4, 128 - 2 * E},
+      {"opt63_b", k_pair_split<E, 4, 0, 2, false, 63>, 128, 4, 128 - 2 * E},
+      {"opt39_b", k_pair_split<E, 4, 0, 2, false, 39>, 128, 4, 128 - 2 * E},
+  };
+#elif defined(PB_SET_OCC)
+  // -DPB_SET_OCC: workgroups per CU the segment height is sized for (1, 2: the
+  // latency-bound rate of one / two waves per SIMD; 6, 8: three / four waves)
+  std::vector<Variant> vs = {
+      {"opt15_w4", k_pair_split<E, 4, 0, 2, false, 15>, 128, 4, 128 - 2 * E},
+      {"opt15_w1", k_pair_split<E, 4, 0, 2, false, 15>, 128, 1, 128 - 2 * E},
+      {"opt15_w2", k_pair_split<E, 4, 0, 2, false, 15>, 128, 2, 128 - 2 * E},
+      {"opt15_w6", k_pair_split<E, 4, 0, 2, false, 15>, 128, 6, 128 - 2 * E},
+      {"opt15_w8", k_pair_split<E, 4, 0, 2, false, 15>, 128, 8, 128 - 2 * E},
+      {"opt7_w8", k_pair_split<E, 4, 0, 2, false, 7>, 128, 8, 128 - 2 * E},
+      {"opt63_w6", k_pair_split<E, 4, 0, 2, false, 63>, 128, 6, 128 - 2 * E},
+      {"opt63_w4", k_pair_split<E, 4, 0, 2, false, 63>, 128, 4, 128 - 2 * E},
+      {"opt15_w4b", k_pair_split<E, 4, 0, 2, false, 15>, 128, 4, 128 - 2 * E},
+  };
+#elif defined(PB_SET_PI)
+  // -DPB_SET_PI: OPT 15 / 63 against 79 / 95 (row pairs' levels interleaved)
+  std::vector<Variant> vs = {
+      {"opt15", k_pair_split<E, 4, 0, 2, false, 15>, 128, 4, 128 - 2 * E},
+      {"opt63", k_pair_split<E, 4, 0, 2, false, 63>, 128, 4, 128 - 2 * E},
+      {"opt79", k_pair_split<E, 4, 0, 2, false, 79>, 128, 4, 128 - 2 * E},
+      {"opt95", k_pair_split<E, 4, 0, 2, false, 95>, 128, 4, 128 - 2 * E},
+      {"opt15_b", k_pair_split<E, 4, 0, 2, false, 15>, 128, 4, 128 - 2 * E},
+      {"opt63_b", k_pair_split<E, 4, 0, 2, false, 63>, 128, 4, 128 - 2 * E},
+      {"opt79_b", k_pair_split<E, 4, 0, 2, false, 79>, 128, 4, 128 - 2 * E},
+      {"opt95_b", k_pair_split<E, 4, 0, 2, false, 95>, 128, 4, 128 - 2 * E},
+  };
+#elif defined(PB_SET_ABL)
+  // -DPB_SET_ABL: ablations of OPT 15 (nlh_pair.h ABL bits; results not
+  // meaningful): 4 no LDS window reads, 8 no s_barrier, 64 no vmcnt waits,
+  // 72 neither, 2 no HBM traffic, 452 VALU only
+  std::vector<Variant> vs = {
+      {"abl0", k_pair_split<E, 4, 0, 2, false, 15>, 128, 4, 128 - 2 * E},
+      {"abl4", k_pair_split<E, 4, 4, 2, false, 15>, 128, 4, 128 - 2 * E},
+      {"abl8", k_pair_split<E, 4, 8, 2, false, 15>, 128, 4, 128 - 2 * E},
+      {"abl64", k_pair_split<E, 4, 64, 2, false, 15>, 128, 4, 128 - 2 * E},
+      {"abl72", k_pair_split<E, 4, 72, 2, false, 15>, 128, 4, 128 - 2 * E},
+      {"abl2", k_pair_split<E, 4, 2, 2, false, 15>, 128, 4, 128 - 2 * E},
+      {"abl452", k_pair_split<E, 4, 452, 2, false, 15>, 128, 4, 128 - 2 * E},
+      {"abl460", k_pair_split<E, 4, 460, 2, false, 15>, 128, 4, 128 - 2 * E},
+  };
+#elif defined(PB_SET_TAIL)
+  // -DPB_SET_TAIL: OPT 15 (round 4), 31 (head), 95 (head + interleave), 223 (+ tail)
+  std::vector<Variant> vs = {
+      {"opt15", k_pair_split<E, 4, 0, 2, false, 15>, 128, 4, 128 - 2 * E},
+      {"opt31", k_pair_split<E, 4, 0, 2, false, 31>, 128, 4, 128 - 2 * E},
+      {"opt95", k_pair_split<E, 4, 0, 2, false, 95>, 128, 4, 128 - 2 * E},
+      {"opt223", k_pair_split<E, 4, 0, 2, false, 223>, 128, 4, 128 - 2 * E},
+      {"opt159", k_pair_split<E, 4, 0, 2, false, 159>, 128, 4, 128 - 2 * E},
+  };
+#elif defined(PB_SET_DEPTH)
+  // -DPB_SET_DEPTH: DMA rows in flight (D) under OPT 223, barrier block 2
+  std::vector<Variant> vs = {
+      {"opt223_D4", k_pair_split<E, 4, 0, 2, false, 223>, 128, 4, 128 - 2 * E},
+      {"opt223_D6", k_pair_split<E, 6, 0, 2, false, 223>, 128, 4, 128 - 2 * E},
+      {"opt223_D8", k_pair_split<E, 8, 0, 2, false, 223>, 128, 4, 128 - 2 * E},
+      {"opt223_D12", k_pair_split<E, 12, 0, 2, false, 223>, 128, 4, 128 - 2 * E},
+      {"opt15_D4", k_pair_split<E, 4, 0, 2, false, 15>, 128, 4, 128 - 2 * E},
+      {"opt15_D8", k_pair_split<E, 8, 0, 2, false, 15>, 128, 4, 128 - 2 * E},
+  };
+#elif defined(PB_SET_LEAN)
+  // -DPB_SET_LEAN: OPT 15, 95, 223 against the lean periods 351 (95|256), 479 (223|256)
+  std::vector<Variant> vs = {
+      {"opt15", k_pair_split<E, 4, 0, 2, false, 15>, 128, 4, 128 - 2 * E},
+      {"opt95", k_pair_split<E, 4, 0, 2, false, 95>, 128, 4, 128 - 2 * E},
+      {"opt223", k_pair_split<E, 4, 0, 2, false, 223>, 128, 4, 128 - 2 * E},
+      {"opt351", k_pair_split<E, 4, 0, 2, false, 351>, 128, 4, 128 - 2 * E},
+      {"opt479", k_pair_split<E, 4, 0, 2, false, 479>, 128, 4, 128 - 2 * E},
+      {"opt415", k_pair_split<E, 4, 0, 2, false, 415>, 128, 4, 128 - 2 * E},
+  };
+#elif defined(PB_SET_NOP)
+  // -DPB_SET_NOP: OPT 223 with eight s_nop per row added on wave 0 (4096) or
+  // wave 1 (8192): what non-VALU instructions on each role's path cost
+  std::vector<Variant> vs = {
+      {"opt223", k_pair_split<E, 4, 0, 2, false, 223>, 128, 4, 128 - 2 * E},
+      {"opt223_nop0", k_pair_split<E, 4, 4096, 2, false, 223>, 128, 4, 128 - 2 * E},
+      {"opt223_nop1", k_pair_split<E, 4, 8192, 2, false, 223>, 128, 4, 128 - 2 * E},
+      {"opt223_nop01", k_pair_split<E, 4, 12288, 2, false, 223>, 128, 4, 128 - 2 * E},
+  };
+#elif defined(PB_SET_W0)
+  // -DPB_SET_W0: wave 0 (stage 1) is the critical role under OPT 223
+  // (profiles/r05/nop): its priority (8 off: 215; 512: wave 0 at priority 3
+  // instead of wave 1: 735) and stage-1 lean periods (256: 479, 471, 991)
+  std::vector<Variant> vs = {
+      {"opt223", k_pair_split<E, 4, 0, 2, false, 223>, 128, 4, 128 - 2 * E},
+      {"opt215", k_pair_split<E, 4, 0, 2, false, 215>, 128, 4, 128 - 2 * E},
+      {"opt735", k_pair_split<E, 4, 0, 2, false, 735>, 128, 4, 128 - 2 * E},
+      {"opt479", k_pair_split<E, 4, 0, 2, false, 479>, 128, 4, 128 - 2 * E},
+      {"opt471", k_pair_split<E, 4, 0, 2, false, 471>, 128, 4, 128 - 2 * E},
+      {"opt991", k_pair_split<E, 4, 0, 2, false, 991>, 128, 4, 128 - 2 * E},
+  };
+#elif defined(PB_SET_PRIO)
   // -DPB_SET_PRIO: OPT 7 (before) against 15 (wave 1 at priority 3), interleaved
   std::vector<Variant> vs = {
       {"opt7", k_pair_split<E, 4, 0, 2, false, 7>, 128, 4, 128 - 2 * E},
@@ -128,8 +253,13 @@ int main(int argc, char **argv) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  for (size_t vi = 0; vi < vs.size(); ++vi) {
-    const Variant &v = vs[vi];
+  // PB_REPS=R: the whole variant list R times over (interleaved A/B; the
+  // first variant of the first round is the bitwise reference)
+  const int reps = std::getenv("PB_REPS") ? std::max(1, std::atoi(std::getenv("PB_REPS"))) : 1;
+  const size_t nv = vs.size();
+  for (size_t vr = 0; vr < nv * (size_t)reps; ++vr) {
+    const size_t vi = vr;
+    const Variant &v = vs[vr % nv];
     // segment height: minimise rounds x (seg + 3E) over the resident slots
     const int nstrip = (int)ceil_div(n, v.strip_out);
     int seg = seg_force;
@@ -176,6 +306,17 @@ int main(int argc, char **argv) {
         cur = 1 - cur;
       }
     };
+#if defined(PB_SET_TRACE)
+    // every launch of an ABL 2048 variant writes its per-wave records through
+    // Rc.lw: the buffer exists before the first launch (round 5: a launch with
+    // lw still null faulted the GPU)
+    uint64_t *dtr = nullptr;
+    const size_t nrec = (size_t)L.nwork * 2 * 4;
+    CK(hipMalloc(&dtr, nrec * 8));
+    CK(hipMemset(dtr, 0, nrec * 8));
+    L.r[0].lw = reinterpret_cast<const double *>(dtr);
+    if (!L.r[0].lw) std::abort();
+#endif
     launch(4);  // check pass count: identical for every variant
     CK(hipDeviceSynchronize());
     CK(hipMemcpy2D(got.data(), (size_t)n * 8, origin(buf[cur]), pitch * 8, (size_t)n * 8, n, hipMemcpyDeviceToHost));
@@ -187,6 +328,61 @@ int main(int argc, char **argv) {
       same = std::memcmp(ref.data(), got.data(), ref.size() * 8) == 0;
       for (size_t i = 0; i < ref.size(); ++i) maxd = std::max(maxd, std::fabs(ref[i] - got[i]));
     }
+#if defined(PB_SET_TRACE)
+    {
+      launch(20);
+      CK(hipDeviceSynchronize());
+      std::vector<uint64_t> tr(nrec);
+      CK(hipMemcpy(tr.data(), dtr, nrec * 8, hipMemcpyDeviceToHost));
+      const char *dir = std::getenv("PB_TRACE_DIR");
+      std::string fn = std::string(dir ? dir : ".") + "/pair_trace_" + v.name + ".csv";
+      FILE *f = std::fopen(fn.c_str(), "w");
+      uint64_t t0 = ~0ull, t1 = 0, tmaxin = 0, tminout = ~0ull;
+      double dsum = 0;
+      int same_simd_role = 0, mixed = 0;
+      std::vector<int> simd_role(8 * 64 * 4 * 4 * 2, 0);  // xcc, se*16+cu.. coarse key below
+      if (f) std::fprintf(f, "block,wave,xcc,se,sh,cu,simd,wave_slot,t_entry,t_exit\n");
+      // key (xcc, se, sh, cu, simd) -> roles seen
+      std::vector<std::pair<uint64_t, int>> keys;
+      for (int bidx = 0; bidx < L.nwork; ++bidx)
+        for (int w = 0; w < 2; ++w) {
+          const uint64_t *r = &tr[(size_t)(2 * bidx + w) * 4];
+          const uint32_t hw = (uint32_t)r[0], xcc = (uint32_t)r[1] & 15;
+          const int simd = (hw >> 4) & 3, cu = (hw >> 8) & 15, sh = (hw >> 12) & 1, se = (hw >> 13) & 7,
+                    ws = hw & 15;
+          if (f) std::fprintf(f, "%d,%d,%u,%d,%d,%d,%d,%d,%llu,%llu\n", bidx, w, xcc, se, sh, cu, simd, ws,
+                              (unsigned long long)r[2], (unsigned long long)r[3]);
+          t0 = std::min(t0, r[2]);
+          t1 = std::max(t1, r[3]);
+          tmaxin = std::max(tmaxin, r[2]);
+          tminout = std::min(tminout, r[3]);
+          dsum += (double)(r[3] - r[2]);
+          keys.push_back({((uint64_t)xcc << 20) | ((uint64_t)se << 12) | ((uint64_t)sh << 8) | ((uint64_t)cu << 4) |
+                              (uint64_t)simd,
+                          w});
+        }
+      if (f) std::fclose(f);
+      std::sort(keys.begin(), keys.end());
+      for (size_t a = 0; a < keys.size();) {
+        size_t b2 = a;
+        int n0 = 0, n1 = 0;
+        while (b2 < keys.size() && keys[b2].first == keys[a].first) {
+          (keys[b2].second ? n1 : n0)++;
+          ++b2;
+        }
+        if (n0 && n1) ++mixed;
+        else ++same_simd_role;
+        a = b2;
+      }
+      // s_memrealtime ticks at 100 MHz
+      std::printf("{\"trace\": \"%s\", \"wgs\": %d, \"span_us\": %.2f, \"last_entry_us\": %.2f, "
+                  "\"first_exit_us\": %.2f, \"mean_wave_us\": %.2f, \"simds_mixed_roles\": %d, "
+                  "\"simds_one_role\": %d}\n",
+                  v.name, L.nwork, (t1 - t0) / 100.0, (tmaxin - t0) / 100.0, (tminout - t0) / 100.0,
+                  dsum / (2.0 * L.nwork) / 100.0, mixed, same_simd_role);
+      std::fflush(stdout);
+    }
+#endif
     launch(20);
     float best_ms = 1e30f;
     for (int r = 0; r < 3; ++r) {
@@ -199,10 +395,14 @@ int main(int argc, char **argv) {
       best_ms = std::min(best_ms, ms);
     }
     const double us = best_ms * 1e3 / passes;
-    std::printf("{\"variant\": \"%s\", \"n\": %d, \"seg\": %d, \"wgs\": %d, \"us_per_pass\": %.2f, "
+    std::printf("{\"rep\": %d, \"variant\": \"%s\", \"n\": %d, \"seg\": %d, \"wgs\": %d, \"us_per_pass\": %.2f, "
                 "\"us_per_step\": %.2f, \"gnode_s\": %.1f, \"bitwise_vs_first\": %s, \"maxdiff\": %.3g}\n",
-                v.name, n, seg, L.nwork, us, us / 2, 2.0 * n * n / us / 1e3, same ? "true" : "false", maxd);
+                (int)(vr / nv), v.name, n, seg, L.nwork, us, us / 2, 2.0 * n * n / us / 1e3, same ? "true" : "false", maxd);
     std::fflush(stdout);
+#if defined(PB_SET_TRACE)
+    CK(hipDeviceSynchronize());
+    CK(hipFree(dtr));
+#endif
   }
   return 0;
 }
