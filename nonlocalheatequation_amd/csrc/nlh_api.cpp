@@ -170,6 +170,7 @@ constexpr EnvKnob kEnvKnobs[] = {
     {"NLH_PITCH_PAD", 0, 1024},    // extra doubles per padded row
     {"NLH_BAND_SEG", 0, 1 << 20},  // edge-band segment height (0 = automatic)
     {"NLH_COMM_INIT_TIMEOUT", 1, 86400},  // seconds a communicator init may take (default 300)
+    {"NLH_SYNC", 0, 3},            // host waits: 0 spin (default), 1 yield, 2 blocking, 3 HIP's auto
 };
 constexpr const char *kRemovedKnobs[] = {"NLH_ABLATE", "NLH_PAIR_ABLATE"};
 
@@ -1017,6 +1018,19 @@ int create_impl(const nlh_params *pin, nlh_solver *s, ncclComm_t reuse_comm = nu
     HIP_TRY(hipGetDevice(&s->device));
   }
   HIP_TRY(hipSetDevice(s->device));
+  // host waits (nlh_synchronize, event waits) spin by default: a blocking or
+  // yielding wait wakes tens of microseconds after the GPU finishes, ~4% of
+  // a 20-step C2 run (r05).  Only a device whose context is not yet active
+  // takes the flag; otherwise HIP keeps what it has (error cleared)
+  {
+    int mode = 0;
+    if (const char *v = std::getenv("NLH_SYNC"))
+      if (*v) mode = std::atoi(v);
+    const unsigned fl = mode == 1 ? hipDeviceScheduleYield
+                        : mode == 2 ? hipDeviceScheduleBlockingSync
+                        : mode == 3 ? hipDeviceScheduleAuto : hipDeviceScheduleSpin;
+    if (hipSetDeviceFlags(fl) != hipSuccess) (void)hipGetLastError();
+  }
   hipDeviceProp_t prop;
   HIP_TRY(hipGetDeviceProperties(&prop, s->device));
   std::snprintf(s->arch, sizeof(s->arch), "%s", prop.gcnArchName);

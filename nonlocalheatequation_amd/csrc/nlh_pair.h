@@ -75,11 +75,15 @@ constexpr int kPairSplitB = 4;  // k_pair_split: rows per barrier
 // the stage-1 wave and nothing on the stage-2 wave -- wave 0 is the critical
 // role under the wave priority, so work off its path pays.  Medians over
 // interleaved repetitions on one box: 15|16|64|128 69.84 us, |256 68.53
-// (E = 8 only: measured there; the lean stage 2 makes hipcc spill).
+// (E = 8 only: measured there; the lean stage 2 makes hipcc spill).  2048 =
+// rings whose slot counts divide the period (production; E = 8: 27.7 KB of
+// LDS per workgroup, 4 per CU): 67.62 -> 66.44 us (profiles/r05/pair/ring_*).
+// 512 (harness only) puts wave 0 at the wave priority instead of wave 1;
+// 1024 (harness only) the lean stage 2 (spills).
 constexpr int kPairPadRows = 16;
 __host__ __device__ constexpr bool pair_rows(int E);
 __host__ __device__ constexpr int pair_opt(int E) {
-  return E == 8 ? 15 | 16 | 64 | 128 | 256
+  return E == 8 ? 15 | 16 | 64 | 128 | 256 | 2048
                 : (E == 13 ? 14 | 16 : (E <= 12 && pair_rows(E) ? 15 | 16 | 64 : 15 | 16));
 }
 
@@ -312,6 +316,12 @@ __host__ __device__ constexpr int pair_tail_c(int E) {
   // (seg + 4E) mod period at the C2 segment height of each E
   return E == 8 ? 4 : -1;
 }
+// the least divisor of P that is >= lo (OPT & 2048's u^{t+1} ring)
+__host__ __device__ constexpr int pair_ring_divisor(int P, int lo) {
+  for (int d = lo; d <= P; ++d)
+    if (P % d == 0) return d;
+  return P;
+}
 __host__ __device__ constexpr int pair_tail_len(int E, int c) {
   const int P = pair_slots(E);
   int x = ((c % P) + P) % P;
@@ -365,10 +375,16 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
   constexpr int RW = W1 + 2 * E;
   constexpr int NCH = RW / 2;
   constexpr int DT = B + D;             // rows fetched ahead of wave 0's row
-  constexpr int K = pow2_ceil(DT + B);  // rows i .. i+DT+B-1 live at once
+  // OPT & 2048 (production): rings whose slot counts divide the period, so
+  // every period starts at slot 0 and a row's ring slots are template
+  // constants (LDS offsets in the instructions, no slot arithmetic per row):
+  // the u^t ring holds one period (K = P >= DT + B rows), the u^{t+1} ring the
+  // least divisor of P that holds its 2B live rows
+  constexpr bool RP = (OPT & 2048) != 0 && !TEST && P >= DT + B;
+  constexpr int K = RP ? P : pow2_ceil(DT + B);  // rows i .. i+DT+B-1 live at once
   constexpr int G = (NCH + 63) / 64;
   constexpr int U1W = W1 + 2 * E + 2;
-  constexpr int U1R = 2 * B;            // u^{t+1} ring rows
+  constexpr int U1R = RP ? pair_ring_divisor(P, 2 * B) : 2 * B;  // u^{t+1} ring rows
   // TEST: L_h[W0] row of the stage-1 columns x0-E .. x0-E+W1-1, staged from
   // the even column at or before x0-E (16-byte DMA chunks)
   constexpr int LOFF = E & 1;
@@ -387,6 +403,11 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
   double *const qbuf = u1buf + U1R * U1W;  // TEST: (dt/alpha) b(t+1) of the u^{t+1} rows
   double *const lwr = qbuf + U1R * U1W;    // TEST: L_h[W0] rows, slots of the u^t ring
   double *const syr = lwr + K * LWW;       // TEST: sin(2 pi y dh) pairs, same slots
+  // ring slots: bsv = b mod K (0 with RP), q = the row's place in the period
+  auto kslot = [](int bsv, int q) __attribute__((always_inline)) { return RP ? q % K : (bsv + q) & (K - 1); };
+  auto uslot = [](int m, int qm) __attribute__((always_inline)) {
+    return RP ? ((qm % U1R) + U1R) % U1R : m & (U1R - 1);
+  };
 
   const int lane = (int)(threadIdx.x & 63);
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -486,8 +507,8 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
         // block is a template constant): a block's first row also reads the
         // second row's window, which the last barrier already published
         double (&w)[NW] = wr[q & 1];
-        if constexpr (!PF || (q & 1) == 0) window(ring + ((bs + q) & (K - 1)) * RW + R * lane, w);
-        if constexpr (PF && (q & 1) == 0) window(ring + ((bs + q + 1) & (K - 1)) * RW + R * lane, wr[1]);
+        if constexpr (!PF || (q & 1) == 0) window(ring + kslot(bs, q) * RW + R * lane, w);
+        if constexpr (PF && (q & 1) == 0) window(ring + kslot(bs, q + 1) * RW + R * lane, wr[1]);
         if constexpr (PI) {
           if constexpr ((q & 1) == 0)
             pair_levels2<E, pair_head_lmax<E, LO, HI>(), pair_head_lmax<E, RB::LON, RB::HIN>()>(wr[0], wr[1],
@@ -503,7 +524,7 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
           double v1 = mcol[1] * acc[1][so];
           double q0 = 0.0, q1 = 0.0;
           if constexpr (TEST) {
-            const int slot = (bs + q) & (K - 1);  // u^t row i: its L_h[W0] / sin rows
+            const int slot = kslot(bs, q);  // u^t row i: its L_h[W0] / sin rows
             const double syv = syr[2 * slot + (sy_idx(m) & 1)];
             const double *lrow = lwr + slot * LWW + LOFF + R * lane;
             const double w00 = sxv[0] * syv, w01 = sxv[1] * syv;
@@ -527,9 +548,9 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
           if constexpr ((ABL & 16) != 0)
             asm volatile("" ::"v"(v0), "v"(v1));  // ablation: no u^{t+1} LDS write
           else
-            *reinterpret_cast<double2 *>(u1buf + (m & (U1R - 1)) * U1W + R * lane) = make_double2(v0, v1);
+            *reinterpret_cast<double2 *>(u1buf + uslot(m, q - 2 * E) * U1W + R * lane) = make_double2(v0, v1);
           if constexpr (TEST)
-            *reinterpret_cast<double2 *>(qbuf + (m & (U1R - 1)) * U1W + R * lane) = make_double2(q0, q1);
+            *reinterpret_cast<double2 *>(qbuf + uslot(m, q - 2 * E) * U1W + R * lane) = make_double2(q0, q1);
         }
         if constexpr ((ABL & 4096) != 0)
           asm volatile("s_nop 0\n\ts_nop 0\n\ts_nop 0\n\ts_nop 0\n\ts_nop 0\n\ts_nop 0\n\ts_nop 0\n\ts_nop 0");
@@ -659,7 +680,7 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
     // fetch + barrier only.  Peeled, so the accumulators never sit under a
     // branch (a conditional scatter makes the compiler copy them around)
     for (int i = 0; i < P; ++i) {
-      issue((i + DT) & (K - 1));
+      issue(RP ? (i + DT < K ? i + DT : i + DT - K) : (i + DT) & (K - 1));
       block_end(i);
     }
     int bs = P & (K - 1);  // b % K
@@ -676,15 +697,15 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
         const int i = b + q;
         if constexpr ((ABL & 32) == 0 && !RB::LEAN)
           if (i > i_last) return;
-        issue((bs + q + DT) & (K - 1));  // u^t row i+DT (clamped; never a slot wave 0 still reads)
+        issue(kslot(bs, q + DT));  // u^t row i+DT (clamped; never a slot wave 0 still reads)
         // u^{t+1} row m2 = i - 2E - B (m2 mod P == q2); rows m2 < 0 are LDS
         // garbage that only reaches accumulators of rows never emitted, each
         // assigned afresh before use
         const int m2 = i - 2 * E - B;
         // OPT & 32: u^{t+1} row m2+1 was written by wave 0 in the previous block
         double (&w2)[NW] = wr[q & 1];
-        if constexpr (!PF || (q & 1) == 0) window(u1buf + (m2 & (U1R - 1)) * U1W + R * lane, w2);
-        if constexpr (PF && (q & 1) == 0) window(u1buf + ((m2 + 1) & (U1R - 1)) * U1W + R * lane, wr[1]);
+        if constexpr (!PF || (q & 1) == 0) window(u1buf + uslot(m2, q - 2 * E - B) * U1W + R * lane, w2);
+        if constexpr (PF && (q & 1) == 0) window(u1buf + uslot(m2 + 1, q + 1 - 2 * E - B) * U1W + R * lane, wr[1]);
         if constexpr (PI) {
           static_assert((q2 & 1) == (q & 1), "row pairs follow the barrier blocks");
           if constexpr ((q & 1) == 0)
@@ -695,7 +716,7 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
           pair_scatter<E, q2, PAIRS ? 1 + (q2 & 1) : 0, LO2, HI2>(w2, acc, kc, hs);
         }
         if constexpr (TEST) {  // (dt/alpha) b(t+1) at the centre row of the output
-          const double *qr = qbuf + (m2 & (U1R - 1)) * U1W + R * lane + E;
+          const double *qr = qbuf + uslot(m2, q - 2 * E - B) * U1W + R * lane + E;
           acc[0][q2] += qr[0];
           acc[1][q2] += qr[1];
         }

@@ -67,7 +67,9 @@ __device__ __forceinline__ double rt_wave_prefix(double x) {
 // CPL: output columns per lane (strips of 64 CPL columns); the lane's CPL
 // prefix values at each offset are adjacent in LDS (one ds_read2_b64 for two
 // columns), and the staged halo is shared by more columns
-template <int NV, int R, bool TEST, bool SKIP = false, bool RUN = false, int CPL = 1>
+// PEEL: a full block's first and last R - 1 input rows add only the pairs of
+// the outputs within their horizon (groups of 8 rows)
+template <int NV, int R, bool TEST, bool SKIP = false, bool RUN = false, int CPL = 1, bool PEEL = false>
 __global__ __launch_bounds__(64) void k_prefix_rt(RectList L, StepConst C, const int2 *__restrict__ tab) {
   constexpr int NPF = 64 * NV + 2;  // doubles per prefix slot: [0] = P(-1) = 0, [1 + k] = P(k)
   __shared__ __attribute__((aligned(16))) double pf[2][NPF];
@@ -111,7 +113,10 @@ __global__ __launch_bounds__(64) void k_prefix_rt(RectList L, StepConst C, const
   const int rfirst = y0 - E, rend = y0 + nout + E;  // input rows [rfirst, rend)
   double cur[NV], nxt[NV];
   load_row(rfirst, cur);
-  for (int r = rfirst; r < rend; ++r) {
+  // one input row: its prefix row into LDS, then the pairs of outputs
+  // JLO .. JHI (template constants; pairs past the horizon add +0)
+  auto row = [&](int r, auto jlo_c, auto jhi_c) __attribute__((always_inline)) {
+    constexpr int JLO = decltype(jlo_c)::value, JHI = decltype(jhi_c)::value;
     const int s = (r - rfirst) & 1;
     if (r + 1 < rend) load_row(r + 1, nxt);
     // prefix row of input row r into slot s
@@ -141,7 +146,7 @@ __global__ __launch_bounds__(64) void k_prefix_rt(RectList L, StepConst C, const
       }
     } else if (!SKIP || (jlo <= 0 && jhi >= R - 1)) {
 #pragma unroll
-      for (int j = 0; j < R; ++j) {
+      for (int j = JLO; j <= JHI; ++j) {
         const int2 o = t[-j];  // {L, -L - 1}, or {0, 0} past the horizon
 #pragma unroll
         for (int c = 0; c < CPL; ++c) acc[j][c] += cen[o.x + c] - cen[o.y + c];
@@ -159,6 +164,36 @@ __global__ __launch_bounds__(64) void k_prefix_rt(RectList L, StepConst C, const
     asm volatile("" ::: "memory");
 #pragma unroll
     for (int k = 0; k < NV; ++k) cur[k] = nxt[k];
+  };
+  using JAll0 = std::integral_constant<int, 0>;
+  using JAllR = std::integral_constant<int, R - 1>;
+  if (PEEL && nout == R && !RUN && !SKIP) {
+    // a full block: input row t = r - y0 reaches outputs
+    // max(0, t-E) .. min(R-1, t+E); its first R-1 rows (t < R-1-E) and last
+    // R-1 rows (t > E) reach only part of the block.  Those rows run in groups
+    // of PG whose pair ranges are the group's union (template constants), so
+    // the pairs past the horizon -- (R-1)/(2E+R) of all, 14% at eps 96 --
+    // shrink to the groups' rounding
+    constexpr int PG = 8, NG = (R - 1 + PG - 1) / PG;
+    int r = rfirst;
+    static_for<NG>([&](auto gc) __attribute__((always_inline)) {
+      constexpr int g = decltype(gc)::value;
+      constexpr int hi = PG * g + PG - 1 < R - 1 ? PG * g + PG - 1 : R - 2;  // t + E of the group's last row
+#pragma unroll 1
+      for (int k = PG * g; k <= hi; ++k, ++r) row(r, JAll0{}, std::integral_constant<int, hi>{});
+    });
+#pragma unroll 1
+    for (; r <= y0 + E; ++r) row(r, JAll0{}, JAllR{});  // t in [R-1-E, E]: every output
+    static_for<NG>([&](auto gc) __attribute__((always_inline)) {
+      constexpr int g = decltype(gc)::value;
+      constexpr int lo = PG * g + 1;  // t - E of the group's first row
+      constexpr int hi = PG * g + PG - 1 < R - 2 ? PG * g + PG - 1 : R - 2;
+#pragma unroll 1
+      for (int k = PG * g; k <= hi; ++k, ++r) row(r, std::integral_constant<int, lo>{}, JAllR{});
+    });
+  } else {
+#pragma unroll 1
+    for (int r = rfirst; r < rend; ++r) row(r, JAll0{}, JAllR{});
   }
   // u' = alpha (S + kc u) [+ (dt/alpha) b]: u(x, y) from the field
   static_assert(!RUN || CPL == 1, "RUN: one column per lane");

@@ -29,7 +29,7 @@ void prefix_rt_table(int E, const int32_t *lens, int32_t *out) {
 
 template <int NV, bool TEST, int CPL = 1>
 static int launch_nv(const RectList &rl, const StepConst &c, const void *table, hipStream_t st) {
-  hipLaunchKernelGGL((k_prefix_rt<NV, kPrefixRows, TEST, false, false, CPL>), dim3(rl.nwork), dim3(64), 0, st, rl,
+  hipLaunchKernelGGL((k_prefix_rt<NV, kPrefixRows, TEST, false, false, CPL, true>), dim3(rl.nwork), dim3(64), 0, st, rl,
                      c, (const int2 *)table);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : (int)e;

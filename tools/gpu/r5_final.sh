@@ -1,0 +1,35 @@
+#!/bin/bash
+# Round 5, final evidence at the library build the round ends on:
+#   1. the whole GPU suite (parity records) and smoke        -> gpurun_out/r5z/
+#   2. per workload: bench line, rocprofv3 --kernel-trace --stats of the same
+#      command, PMC passes and record (tools/bench_evidence.sh) -> gpurun_out/r5e/<workload>/
+#   3. the driver's 20-step C2 line three times, C3 on one block and as 8
+#      virtual ranks, the weak layouts as 2 / 4 / 8 virtual ranks
+#   bash tools/gpu/r5_final.sh COMMIT
+set -o pipefail
+export TMPDIR=/tmp
+C=${1:-unknown}
+O=gpurun_out/r5z
+E=gpurun_out/r5e
+mkdir -p $O $E
+rm -f gpurun_out/parity_l2.jsonl gpurun_out/parity_nodes.jsonl
+timeout -k 10 1100 python -u -m pytest tests -m gpu -q --maxfail=10 --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1
+rc=$?; echo "pytest rc=$rc" >> $O/pytest_gpu.log
+cp gpurun_out/parity_l2.jsonl gpurun_out/parity_nodes.jsonl $O/ 2>/dev/null
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit 1
+for i in 1 2 3; do
+  timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $E/bench20_$i.json 2> $E/bench20_$i.err || exit 1
+done
+NLH_N=4096 NLH_EPS=8 tools/bench_evidence.sh $E/c2 k_pair_split weak_4096_eps8_prod 33554432 $C -- || exit 1
+NLH_N=4096 NLH_EPS=8 NLH_TEST=1 tools/bench_evidence.sh $E/test k_pair_split weak_4096_eps8_test 33554432 $C -- --test-mode || exit 1
+NLH_N=8192 NLH_EPS=32 tools/bench_evidence.sh $E/c4 k_wide weak_8192_eps32_prod 67108864 $C -- --eps 32 --lattice 8192 --steps 200 || exit 1
+NLH_N=8192 NLH_EPS=96 NLH_STEPS=6 tools/bench_evidence.sh $E/eps96 k_prefix_rt weak_8192_eps96_prod 67108864 $C -- --eps 96 --lattice 8192 --steps 20 || exit 1
+NLH_N=8192 NLH_EPS=300 NLH_STEPS=2 tools/bench_evidence.sh $E/eps300 k_prefix_rt weak_8192_eps300_prod 67108864 $C -- --eps 300 --lattice 8192 --steps 4 --warmup 2 --warmup-ms 0 --no-cpu-baseline || exit 1
+timeout -k 10 300 python bench.py --strong --lattice 32768 --steps 20 --pmc off --no-cpu-baseline > $O/c3_1block.json 2> $O/c3_1block.err || exit 1
+NLH_VIRTUAL_RANKS=8 timeout -k 10 300 python bench.py --strong --lattice 32768 --blocks 2x4 --steps 20 --pmc off --no-cpu-baseline > $O/c3_v8.json 2> $O/c3_v8.err || exit 1
+for b in 2x1 2x2 2x4; do
+  v=$(( ${b%x*} * ${b#*x} ))
+  NLH_VIRTUAL_RANKS=$v timeout -k 10 300 python bench.py --blocks $b --steps 200 --pmc off --no-cpu-baseline > $O/weak_v${v}.json 2> $O/weak_v${v}.err || exit 1
+done
+echo done > $O/done

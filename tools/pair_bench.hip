@@ -209,6 +209,14 @@ int main(int argc, char **argv) {
       {"opt471", k_pair_split<E, 4, 0, 2, false, 471>, 128, 4, 128 - 2 * E},
       {"opt991", k_pair_split<E, 4, 0, 2, false, 991>, 128, 4, 128 - 2 * E},
   };
+#elif defined(PB_SET_RING)
+  // -DPB_SET_RING: OPT 479 (round-5 library) against 2527 (+ period-aligned rings)
+  std::vector<Variant> vs = {
+      {"opt479", k_pair_split<E, 4, 0, 2, false, 479>, 128, 4, 128 - 2 * E},
+      {"opt2527", k_pair_split<E, 4, 0, 2, false, 2527>, 128, 4, 128 - 2 * E},
+      {"opt15", k_pair_split<E, 4, 0, 2, false, 15>, 128, 4, 128 - 2 * E},
+      {"opt2063", k_pair_split<E, 4, 0, 2, false, 2063>, 128, 4, 128 - 2 * E},
+  };
 #elif defined(PB_SET_PRIO)
   // -DPB_SET_PRIO: OPT 7 (before) against 15 (wave 1 at priority 3), interleaved
   std::vector<Variant> vs = {

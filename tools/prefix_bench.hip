@@ -57,6 +57,23 @@ int main(int argc, char **argv) {
   // round 4 (profiles/r04/first/prefix_bench.jsonl): R = 32 without SKIP /
   // RUN was the fastest everywhere (the uniform branches serialise the LDS
   // reads; R 48 / 64 cost occupancy)
+#if defined(PX_SET_PEEL)
+  // -DPX_SET_PEEL: round 5, the partial-horizon rows peeled (PEEL) against the round-4 form
+  std::vector<Variant> vs4 = {
+      {"R32", k_prefix_rt<4, 32, false>, 32},
+      {"R32_peel", k_prefix_rt<4, 32, false, false, false, 1, true>, 32},
+      {"R32_b", k_prefix_rt<4, 32, false>, 32},
+      {"R32_peel_b", k_prefix_rt<4, 32, false, false, false, 1, true>, 32},
+  };
+  std::vector<Variant> vs6 = {
+      {"NV6_R32", k_prefix_rt<6, 32, false>, 32},
+      {"NV6_R32_peel", k_prefix_rt<6, 32, false, false, false, 1, true>, 32},
+  };
+  std::vector<Variant> vs8 = {
+      {"NV8_R32", k_prefix_rt<8, 32, false>, 32},
+      {"NV8_R32_peel", k_prefix_rt<8, 32, false, false, false, 1, true>, 32},
+  };
+#else
   std::vector<Variant> vs4 = {
       {"R32", k_prefix_rt<4, 32, false>, 32},
       {"R32_cpl2_nv6", k_prefix_rt<6, 32, false, false, false, 2>, 32, 2},
@@ -76,6 +93,7 @@ int main(int argc, char **argv) {
       {"R32_run", k_prefix_rt<8, 32, false, false, true>, 32},
       {"R48_run", k_prefix_rt<8, 48, false, false, true>, 48},
   };
+#endif
   for (int E : eps) {
     const int H = E, XL = (E + 7) / 8 * 8;
     const int64_t pitch = (XL + ceil_div(n, 64) * 64 + 512 + 7) / 8 * 8;
