@@ -83,7 +83,7 @@ constexpr int kPairSplitB = 4;  // k_pair_split: rows per barrier
 constexpr int kPairPadRows = 16;
 __host__ __device__ constexpr bool pair_rows(int E);
 __host__ __device__ constexpr int pair_opt(int E) {
-  return E == 8 ? 15 | 16 | 64 | 128 | 256 | 2048
+  return E == 8 ? 15 | 16 | 64 | 128 | 256 | 2048 | 4096
                 : (E == 13 ? 14 | 16 : (E <= 12 && pair_rows(E) ? 15 | 16 | 64 : 15 | 16));
 }
 
@@ -537,10 +537,16 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
             if (mcol[1] == 0.0) v1 = 0.0;
           }
           if constexpr (RB::LEAN) {
-            // lean rows: a select (v_cndmask on a wave-uniform condition), no branch
-            const bool out = gy < 0 || gy >= gny;
-            v0 = out ? 0.0 : v0;
-            v1 = out ? 0.0 : v1;
+            // lean rows: a select (v_cndmask on a wave-uniform condition), no
+            // branch.  OPT & 4096: only the first 3E - P rows of a period take
+            // it -- a lean period starts at b >= P, so its rows q >= 3E - P lie
+            // past the segment's first E u^{t+1} rows, and lean periods end
+            // before its last E (the only rows that can leave the lattice)
+            if constexpr ((OPT & 4096) == 0 || q < 3 * E - P) {
+              const bool out = gy < 0 || gy >= gny;
+              v0 = out ? 0.0 : v0;
+              v1 = out ? 0.0 : v1;
+            }
           } else if (gy < 0 || gy >= gny) {
             v0 = 0.0;
             v1 = 0.0;
@@ -587,7 +593,9 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
     constexpr bool LEANOK = (OPT & 256) != 0 && HEAD && (P % B) == 0 && (ABL & 32) == 0;
     static_assert(!LEANOK || P >= 2 * E, "lean periods start past the warm-up");
     if constexpr (LEANOK) {
-      for (; b + P <= bend; b += P) {
+      // OPT & 4096: lean periods end before the segment's last E u^{t+1} rows
+      const int lean_end = (OPT & 4096) != 0 ? min(bend, n_in - E) : bend;
+      for (; b + P <= lean_end; b += P) {
         static_for<P>([&](auto qc) __attribute__((always_inline)) {
           body(qc, PairRowBounds<-E, E, -E, E, true>{});
         });
@@ -784,7 +792,9 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
     // j the stores of iterations j-D+1 .. j have been issued (j-D+1 >= 4E+B)
     static_assert(!LEANOK || (2 * P - 2 * E - B >= 2 * E && 2 * P + B - D >= 4 * E + B), "lean from b = 2P");
     if constexpr (LEANOK) {
-      for (; b + P <= bend; b += P) {
+      // OPT & 4096: lean periods end before the segment's last E u^{t+1} rows
+      const int lean_end = (OPT & 4096) != 0 ? min(bend, n_in - E) : bend;
+      for (; b + P <= lean_end; b += P) {
         static_for<P>([&](auto qc) __attribute__((always_inline)) {
           body(qc, PairRowBounds<-E, E, -E, E, true>{});
         });

@@ -358,6 +358,10 @@ def test_driver_balances_large_tiles(tmp_path):
     cnt = np.bincount(np.array(grid).ravel(), minlength=R)
     assert cnt.min() >= 1 and all(0 <= r <= 10000 for r in rates) and sum(rates) <= 10000 * 1.001, (rates, cnt)
     assert lines[j + 1 + npx] == "Load balanced correctly", (rates, cnt)
+    # the reference's verdict (|rate - mean| <= 1500) is loose once the four
+    # owners share one GPU (rates ~2000-2500): the spread itself
+    # must be small -- max / min <= 1.5 (r04: 2410 / 1823 = 1.32)
+    assert max(rates) <= 1.5 * min(rates), (rates, cnt)
     m = re.search(r"^l2: (\S+) linfinity: (\S+)$", out.stdout, re.M)
     assert m and float(m.group(1)) / (n * n) <= 1e-6
 

@@ -2,7 +2,7 @@
 # Round 5, final evidence at the library build the round ends on:
 #   1. the whole GPU suite (parity records) and smoke        -> gpurun_out/r5z/
 #   2. per workload: bench line, rocprofv3 --kernel-trace --stats of the same
-#      command, PMC passes and record (tools/bench_evidence.sh) -> gpurun_out/r5e/<workload>/
+#      command, PMC passes and record (tools/bench_evidence.sh) -> gpurun_out/r5v/<workload>/
 #   3. the driver's 20-step C2 line three times, C3 on one block and as 8
 #      virtual ranks, the weak layouts as 2 / 4 / 8 virtual ranks
 #   bash tools/gpu/r5_final.sh COMMIT
@@ -10,7 +10,7 @@ set -o pipefail
 export TMPDIR=/tmp
 C=${1:-unknown}
 O=gpurun_out/r5z
-E=gpurun_out/r5e
+E=gpurun_out/r5v
 mkdir -p $O $E
 rm -f gpurun_out/parity_l2.jsonl gpurun_out/parity_nodes.jsonl
 timeout -k 10 1100 python -u -m pytest tests -m gpu -q --maxfail=10 --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1

@@ -216,6 +216,7 @@ int main(int argc, char **argv) {
       {"opt2527", k_pair_split<E, 4, 0, 2, false, 2527>, 128, 4, 128 - 2 * E},
       {"opt15", k_pair_split<E, 4, 0, 2, false, 15>, 128, 4, 128 - 2 * E},
       {"opt2063", k_pair_split<E, 4, 0, 2, false, 2063>, 128, 4, 128 - 2 * E},
+      {"opt6623", k_pair_split<E, 4, 0, 2, false, 6623>, 128, 4, 128 - 2 * E},
   };
 #elif defined(PB_SET_PRIO)
   // -DPB_SET_PRIO: OPT 7 (before) against 15 (wave 1 at priority 3), interleaved
