@@ -65,7 +65,8 @@ enum nlh_influence { NLH_INFLUENCE_CONSTANT = 0, NLH_INFLUENCE_LINEAR = 1 };
  * same J=1 disk sum from row windows, O(eps) adds per node instead of the
  * N(eps) terms: nested windows for eps 1..16 (two-step k_pair_split, k_fast)
  * and 36..64 (compile-time k_wide instances), prefix-sum windows for 17..35
- * (k_wide), and past 64 a run-time-horizon prefix-window kernel (k_prefix_rt);
+ * (k_wide), and past 64 a run-time-horizon prefix-window kernel (k_prefix_rt,
+ * k_prefix_rtc with the window staged in 512-column chunks past eps 224);
  * in test mode the manufactured source comes from a precomputed L_h[W0]
  * field; J = 1 - r runs LDS-tile kernels (k_weighted*) up to eps 52.
  * FAST differs from the reference only by summation rounding: <= 1e-12 of
@@ -77,8 +78,8 @@ enum nlh_influence { NLH_INFLUENCE_CONSTANT = 0, NLH_INFLUENCE_LINEAR = 1 };
  * error is itself at that floor (l2 ~ 1e-20 .. 1e-11: few steps, large
  * eps) the L2 difference is bounded by B instead.
  * AUTO = FAST (production and test mode) except where FAST cannot apply,
- * which runs EXACT: k*dt*dh = 0 past eps 16; eps > 224 (the run-time
- * kernel's 512-column staged window); J = 1 - r past eps 52 (the weighted
+ * which runs EXACT: k*dt*dh = 0 past eps 16; eps > 992 (the chunked
+ * run-time kernel's LDS prefix row); J = 1 - r past eps 52 (the weighted
  * tile past 160 KB of LDS).  An explicit FAST request there is refused.  */
 enum nlh_kernel { NLH_KERNEL_AUTO = 0, NLH_KERNEL_EXACT = 1, NLH_KERNEL_FAST = 2 };
 

@@ -842,7 +842,11 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
 // 8), which the host launches when a list has more workgroups than the device
 // holds at once: with several rounds of workgroups the priority costs 1-4%
 // (C2 harness 16384^2 / 32768^2: 982-991 vs 995-998 / 3861-3871 vs 4016-4027
-// us per pass), in one round it gains 4% (4096^2 / 8192^2; profiles/r04/prio/)
+// us per pass), in one round it gains 4% (4096^2 / 8192^2; profiles/r04/prio/).
+// The no-priority launch also drops the period-aligned rings (2048) and the
+// tail skip (128): with several rounds they cost 4-5% (harness OPT 6615 vs
+// 4439, 16384^2: 1022-1024 vs 979-982, 32768^2: 3998-4009 vs 3794 us per
+// pass; profiles/r05/pair/big*.jsonl); the lattice-edge select stays.
 // Resident workgroups per CU (register/LDS-limited) for the host's choice of
 // segment height; 0 for an unknown variant
 template <int E>
@@ -861,7 +865,7 @@ int pair_blocks_per_cu_e(int variant) {
 
 template <int E>
 int launch_pair_e(const RectList &rl, const StepConst &c, int variant, hipStream_t st) {
-  constexpr int NP = pair_opt(E) & ~8;
+  constexpr int NP = pair_opt(E) & ~(8 | 128 | 2048);
   if (variant == 1)
     hipLaunchKernelGGL((k_pair_split<E, kPairSplitD>), dim3(rl.nwork), dim3(128), 0, st, rl, c);
   else if (variant == 6)

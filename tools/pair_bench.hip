@@ -218,6 +218,29 @@ int main(int argc, char **argv) {
       {"opt2063", k_pair_split<E, 4, 0, 2, false, 2063>, 128, 4, 128 - 2 * E},
       {"opt6623", k_pair_split<E, 4, 0, 2, false, 6623>, 128, 4, 128 - 2 * E},
   };
+#elif defined(PB_SET_BIG)
+  // -DPB_SET_BIG: the multi-round regime (16384^2 / 32768^2 as one block, the
+  // host launches without the wave priority): round-4 NP (7) against the
+  // round-5 options without (6615) and with (6623) the priority, and subsets
+  std::vector<Variant> vs = {
+      {"opt7", k_pair_split<E, 4, 0, 2, false, 7>, 128, 4, 128 - 2 * E},
+      {"opt6615", k_pair_split<E, 4, 0, 2, false, 6615>, 128, 4, 128 - 2 * E},
+      {"opt6623", k_pair_split<E, 4, 0, 2, false, 6623>, 128, 4, 128 - 2 * E},
+      {"opt2055", k_pair_split<E, 4, 0, 2, false, 2055>, 128, 4, 128 - 2 * E},
+      {"opt87", k_pair_split<E, 4, 0, 2, false, 87>, 128, 4, 128 - 2 * E},
+      {"opt343", k_pair_split<E, 4, 0, 2, false, 343>, 128, 4, 128 - 2 * E},
+  };
+#elif defined(PB_SET_BIG2)
+  // -DPB_SET_BIG2: the same regime, 343 (no period-aligned rings) with the tail
+  // skip (128), the lattice-edge select (4096) and the priority (8) added
+  std::vector<Variant> vs = {
+      {"opt343", k_pair_split<E, 4, 0, 2, false, 343>, 128, 4, 128 - 2 * E},
+      {"opt471", k_pair_split<E, 4, 0, 2, false, 471>, 128, 4, 128 - 2 * E},
+      {"opt4439", k_pair_split<E, 4, 0, 2, false, 4439>, 128, 4, 128 - 2 * E},
+      {"opt4567", k_pair_split<E, 4, 0, 2, false, 4567>, 128, 4, 128 - 2 * E},
+      {"opt351", k_pair_split<E, 4, 0, 2, false, 351>, 128, 4, 128 - 2 * E},
+      {"opt6615", k_pair_split<E, 4, 0, 2, false, 6615>, 128, 4, 128 - 2 * E},
+  };
 #elif defined(PB_SET_PRIO)
   // -DPB_SET_PRIO: OPT 7 (before) against 15 (wave 1 at priority 3), interleaved
   std::vector<Variant> vs = {
