@@ -171,6 +171,8 @@ constexpr EnvKnob kEnvKnobs[] = {
     {"NLH_BAND_SEG", 0, 1 << 20},  // edge-band segment height (0 = automatic)
     {"NLH_COMM_INIT_TIMEOUT", 1, 86400},  // seconds a communicator init may take (default 300)
     {"NLH_SYNC", 0, 3},            // host waits: 0 spin (default), 1 yield, 2 blocking, 3 HIP's auto
+    {"NLH_PAIR_PRIO", 0, 2},
+    {"NLH_TRACE_REPART", 0, 1},    // repartition phase times on stderr       // k_pair_split wave priority: 0 never, 1 one-round lists, 2 and not on bands
 };
 constexpr const char *kRemovedKnobs[] = {"NLH_ABLATE", "NLH_PAIR_ABLATE"};
 
@@ -286,6 +288,7 @@ struct nlh_solver {
   int pair_test = 5;
   int pair_cu = 4;     // split-kernel workgroups per CU the segments are sized for (NLH_PAIR_CU)
   int64_t pair_resident = 0;  // k_pair_split workgroups the device holds at once (0: not yet asked)
+  int pair_prio = 1;          // NLH_PAIR_PRIO (kEnvKnobs)
   hipStream_t s_main = nullptr, s_comm = nullptr, s_band = nullptr;
   hipEvent_t ev_ready = nullptr, ev_halo = nullptr, ev_band = nullptr, ev_int = nullptr;
   bool halo_fresh = false;  // the current field's halo holds its neighbours' values
@@ -332,6 +335,8 @@ struct nlh_solver {
   // interior, bands and exchange, one per nlh_run)
   int timing = 0;
   std::vector<hipEvent_t> ev_pool;  // pair p = events 2p, 2p + 1
+  double *stage = nullptr;  // repartition staging buffer, kept for the next one (kStageKeepBytes)
+  size_t stage_cap = 0;     // its size in doubles
   size_t ev_used = 0;
   std::vector<EvMeta> ev_meta;      // one per recorded pair
   // pairs already folded into running totals (long windows: completed pairs
@@ -722,7 +727,7 @@ int launch_stencil(nlh_solver *s, RLIter b, RLIter e, hipStream_t st) {
   return NLH_OK;
 }
 
-int launch_pair_lists(nlh_solver *s, RLIter b, RLIter e, hipStream_t st) {
+int launch_pair_lists(nlh_solver *s, RLIter b, RLIter e, hipStream_t st, bool band) {
   for (; b != e; ++b) {
     const nlh::RectList &rl = *b;
     if (rl.nwork == 0) continue;
@@ -732,7 +737,7 @@ int launch_pair_lists(nlh_solver *s, RLIter b, RLIter e, hipStream_t st) {
     if (v == 5 || v == 6) {
       if (s->pair_resident == 0)
         s->pair_resident = (int64_t)std::max(1, nlh::pair_blocks_per_cu((int)s->p.eps, v)) * s->cus;
-      if (rl.nwork > s->pair_resident) v |= nlh::kPairNoPrio;
+      if (rl.nwork > s->pair_resident || s->pair_prio == 0 || (band && s->pair_prio == 2)) v |= nlh::kPairNoPrio;
     }
     const int rc = nlh::launch_pair(rl, s->sc, v, st);
     if (rc != 0) return fail(NLH_ERR_HIP, std::string("pair launch failed: ") + hipGetErrorString((hipError_t)rc));
@@ -818,7 +823,7 @@ int enqueue_step(nlh_solver *s, int nsteps) {
                      hipStream_t st, EvKind kind) {
     const std::vector<nlh::RectList> &v = two ? pr : one;
     auto run = [&](RLIter b, RLIter e) {
-      return two ? launch_pair_lists(s, b, e, st) : launch_stencil(s, b, e, st);
+      return two ? launch_pair_lists(s, b, e, st, kind == kEvBand) : launch_stencil(s, b, e, st);
     };
     bool any = false;
     for (const auto &rl : v) any |= rl.nwork > 0;
@@ -936,6 +941,36 @@ int compute_lw(nlh_solver *s) {
   return NLH_OK;
 }
 
+// NLH_TRACE_REPART=1: one JSON line per repartition on stderr with the host
+// milliseconds of its phases (diagnostics of the balancing cost)
+struct PhaseTrace {
+  bool on = false;
+  std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now(), last = t0;
+  std::string out;
+  void mark(const char *what) {
+    if (!on) return;
+    const auto t = std::chrono::steady_clock::now();
+    char b[64];
+    std::snprintf(b, sizeof b, "%s\"%s\": %.3f", out.empty() ? "" : ", ", what,
+                  std::chrono::duration<double, std::milli>(t - last).count());
+    out += b;
+    last = t;
+  }
+  ~PhaseTrace();
+};
+thread_local PhaseTrace *g_trace = nullptr;  // the repartition in progress (create_impl marks its phases)
+inline void trace_mark(const char *what) {
+  if (g_trace) g_trace->mark(what);
+}
+PhaseTrace::~PhaseTrace() {
+  {
+    if (on)
+      std::fprintf(stderr, "{\"repartition_ms\": {%s}, \"total_ms\": %.3f}\n", out.c_str(),
+                   std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+  }
+  g_trace = nullptr;
+}
+
 // frees every device resource; the communicator too unless keep_comm
 void release_impl(nlh_solver *s, bool keep_comm) {
   (void)hipSetDevice(s->device);
@@ -943,6 +978,7 @@ void release_impl(nlh_solver *s, bool keep_comm) {
   if (s->s_comm) (void)hipStreamSynchronize(s->s_comm);
   if (s->s_band) (void)hipStreamSynchronize(s->s_band);
   if (s->s_copy) (void)hipStreamSynchronize(s->s_copy);
+  trace_mark("r_sync");
   if (s->comm && !keep_comm) ncclCommDestroy(s->comm);
   (void)hipFree(s->snap_dev);
   if (s->snap_host) (void)hipHostFree(s->snap_host);
@@ -954,10 +990,12 @@ void release_impl(nlh_solver *s, bool keep_comm) {
     (void)hipFree(b.base[1]);
     (void)hipFree(b.lw_base);
   }
+  trace_mark("r_blocks");
   for (auto &pr : s->peers) {
     (void)hipFree(pr.send);
     (void)hipFree(pr.recv);
   }
+  trace_mark("r_peers");
   (void)hipFree(s->d_wt);
   (void)hipFree(s->d_qj);
   (void)hipFree(s->d_ptab);
@@ -966,6 +1004,8 @@ void release_impl(nlh_solver *s, bool keep_comm) {
   (void)hipFree(s->d_lens);
   (void)hipFree(s->d_part);
   (void)hipFree(s->d_red);
+  (void)hipFree(s->stage);
+  trace_mark("r_tables");
   for (auto e : s->ev_pool) (void)hipEventDestroy(e);
   if (s->ev_ready) (void)hipEventDestroy(s->ev_ready);
   if (s->ev_halo) (void)hipEventDestroy(s->ev_halo);
@@ -983,8 +1023,24 @@ int destroy_impl(nlh_solver *s) {
   return NLH_OK;
 }
 
-// reuse_comm: an existing communicator over the same ranks (nlh_repartition)
-int create_impl(const nlh_params *pin, nlh_solver *s, ncclComm_t reuse_comm = nullptr) {
+// the streams and events of a solver (swapped between the old and the new
+// solver of a repartition)
+void swap_queues(nlh_solver *a, nlh_solver *b) {
+  std::swap(a->s_main, b->s_main);
+  std::swap(a->s_comm, b->s_comm);
+  std::swap(a->s_band, b->s_band);
+  std::swap(a->ev_ready, b->ev_ready);
+  std::swap(a->ev_halo, b->ev_halo);
+  std::swap(a->ev_band, b->ev_band);
+  std::swap(a->ev_int, b->ev_int);
+  std::swap(a->ev_pool, b->ev_pool);
+}
+
+// reuse_comm: an existing communicator over the same ranks (nlh_repartition);
+// donor: the solver being repartitioned, whose idle streams and events the
+// new one takes over (creating and destroying them was ~13 of ~22 ms per
+// repartition, profiles/r05/repart/)
+int create_impl(const nlh_params *pin, nlh_solver *s, ncclComm_t reuse_comm = nullptr, nlh_solver *donor = nullptr) {
   const nlh_params &p = *pin;
   if (p.nx <= 0 || p.ny <= 0) return fail(NLH_ERR_ARG, "nx, ny must be positive");
   if (p.eps < 1) return fail(NLH_ERR_ARG, "eps must be >= 1");
@@ -1065,6 +1121,7 @@ int create_impl(const nlh_params *pin, nlh_solver *s, ncclComm_t reuse_comm = nu
     if (std::atoi(ps) == 1) s->pair_split = 1;  // k_pair_split with 16-slot rings (variant 1)
   if (const char *pc = std::getenv("NLH_PAIR_CU")) s->pair_cu = std::max(1, std::atoi(pc));
   if (const char *pt = std::getenv("NLH_PAIR_TEST")) s->pair_test = std::atoi(pt) == 0 ? 4 : 5;
+  if (const char *pp = std::getenv("NLH_PAIR_PRIO")) s->pair_prio = std::atoi(pp);
   s->halo = rv.halo;
   s->plan = nlh::make_plan(p.nx, p.ny, s->halo, tx, ty, s->owner, p.split_tiles == 0);
   s->vranks = vranks;
@@ -1074,16 +1131,22 @@ int create_impl(const nlh_params *pin, nlh_solver *s, ncclComm_t reuse_comm = nu
   else
     s->mine.push_back((int)p.rank);
   s->ev_acc_owner.assign(s->owners, 0.0);
+  trace_mark("c_plan");
 
-  HIP_TRY(hipStreamCreateWithFlags(&s->s_main, hipStreamNonBlocking));
-  HIP_TRY(hipStreamCreateWithPriority(&s->s_comm, hipStreamNonBlocking, prio_hi));
-  HIP_TRY(hipStreamCreateWithPriority(&s->s_band, hipStreamNonBlocking, prio_hi));
-  HIP_TRY(hipEventCreateWithFlags(&s->ev_ready, hipEventDisableTiming));
-  HIP_TRY(hipEventCreateWithFlags(&s->ev_halo, hipEventDisableTiming));
-  HIP_TRY(hipEventCreateWithFlags(&s->ev_band, hipEventDisableTiming));
-  HIP_TRY(hipEventCreateWithFlags(&s->ev_int, hipEventDisableTiming));
+  if (donor && donor->s_main) {
+    swap_queues(s, donor);
+  } else {
+    HIP_TRY(hipStreamCreateWithFlags(&s->s_main, hipStreamNonBlocking));
+    HIP_TRY(hipStreamCreateWithPriority(&s->s_comm, hipStreamNonBlocking, prio_hi));
+    HIP_TRY(hipStreamCreateWithPriority(&s->s_band, hipStreamNonBlocking, prio_hi));
+    HIP_TRY(hipEventCreateWithFlags(&s->ev_ready, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&s->ev_halo, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&s->ev_band, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&s->ev_int, hipEventDisableTiming));
+  }
   HIP_TRY(hipEventRecord(s->ev_band, s->s_main));
   HIP_TRY(hipEventRecord(s->ev_int, s->s_main));
+  trace_mark("c_streams");
 
   // ---- constants and host-computed tables (glibc sin, bit-equal to w())
   std::vector<double> sxt(p.nx + 2 * E), syt(p.ny + 2 * E);
@@ -1149,6 +1212,7 @@ int create_impl(const nlh_params *pin, nlh_solver *s, ncclComm_t reuse_comm = nu
   s->sc.ny = p.ny;
   s->sc.E = E;
   set_time(s, 0);
+  trace_mark("c_tables");
 
   // ---- local blocks, padded (see nlh_device.h)
   const int64_t XL = round_up(s->halo, 8);
@@ -1193,11 +1257,13 @@ int create_impl(const nlh_params *pin, nlh_solver *s, ncclComm_t reuse_comm = nu
     s->blocks.push_back(b);
   }
   HIP_TRY(hipStreamSynchronize(s->s_main));
+  trace_mark("c_blocks");
 
   s->exchange_planned = !s->plan.pieces.empty() || s->force_bands;
   int rc = build_rectlists(s, 0);
   if (rc) return rc;
   if (s->pair && (rc = build_rectlists(s, 1))) return rc;
+  trace_mark("c_rectlists");
 
   // ---- RCCL communicator and exchange plan
   if (reuse_comm) {
@@ -1228,8 +1294,10 @@ int create_impl(const nlh_params *pin, nlh_solver *s, ncclComm_t reuse_comm = nu
                                     std::to_string(cr) + "), expected " + std::to_string(want_n) + " (rank " +
                                     std::to_string(want_r) + ")");
   }
+  trace_mark("c_comm");
   rc = build_exchange(s);
   if (rc) return rc;
+  trace_mark("c_exchange");
   if (s->exchange && !s->comm && !s->peers.empty())
     return fail(NLH_ERR_STATE, "internal: peers without communicator");
 
@@ -1305,6 +1373,9 @@ int comm_init_bounded(ncclComm_t *out, int nranks, const ncclUniqueId &id, int r
 // (profiles/r04/{fourth,fifth,sixth}: diag_8192.log, the large-move test).
 // The chunks match pairwise in order on both sides.
 constexpr size_t kP2PChunk = size_t(1) << 25;
+// a repartition's staging buffer stays with the solver for the next one up
+// to this size (tile moves of a few tiles; larger ones are freed after use)
+constexpr size_t kStageKeepBytes = size_t(2) << 30;
 bool p2p(bool send, double *buf, size_t cnt, int peer, ncclComm_t comm, hipStream_t st) {
   for (size_t o = 0; o < cnt; o += kP2PChunk) {
     const size_t c = std::min(kP2PChunk, cnt - o);
@@ -1408,15 +1479,21 @@ int repartition_impl(nlh_solver *s, const std::vector<int32_t> &own) {
   HIP_TRY(hipStreamSynchronize(s->s_comm));
   HIP_TRY(hipStreamSynchronize(s->s_band));
   if (own == s->owner) return NLH_OK;
+  PhaseTrace tr;
+  if (const char *e = std::getenv("NLH_TRACE_REPART")) tr.on = std::atoi(e) != 0;
+  if (tr.on) g_trace = &tr;
   nlh_params p = s->p;
   p.owner = own.data();
   p.comm_id = nullptr;
   if ((rc = repartition_fits(s, own))) return rc;
+  tr.mark("fits_vote");
   nlh_solver *n = new nlh_solver();
-  rc = create_impl(&p, n, s->comm);
+  rc = create_impl(&p, n, s->comm, s);
+  tr.mark("create");
   if (rc) {
     const std::string keep = g_err;
     n->comm = nullptr;  // still the caller's
+    if (!s->s_main) swap_queues(s, n);  // the old solver's streams back
     destroy_impl(n);
     g_err = keep;
     return rc;
@@ -1445,11 +1522,23 @@ int repartition_impl(nlh_solver *s, const std::vector<int32_t> &own) {
   const size_t tb = (size_t)(tw * th);
   const size_t pitch_b = (size_t)tw * sizeof(double);
   int status = NLH_OK;
-  std::vector<double *> bufs;
+  // staging: one buffer for every pack and receive, the old solver's when it
+  // is large enough (kept across repartitions up to kStageKeepBytes)
+  size_t need = 0;
+  for (auto &kv : sends) need += kv.second.size() * tb;
+  for (auto &kv : recvs) need += kv.second.size() * tb;
+  if (need > s->stage_cap) {
+    (void)hipFree(s->stage);
+    s->stage = nullptr;
+    s->stage_cap = 0;
+    if (hipMalloc(&s->stage, need * sizeof(double)) == hipSuccess) s->stage_cap = need;
+    else s->stage = nullptr;
+  }
+  size_t stage_used = 0;
   auto stage = [&](size_t ntiles) -> double * {
-    double *b = nullptr;
-    if (hipMalloc(&b, std::max<size_t>(ntiles * tb, 1) * sizeof(double)) != hipSuccess) return nullptr;
-    bufs.push_back(b);
+    if (!s->stage || stage_used + ntiles * tb > s->stage_cap) return nullptr;
+    double *b = s->stage + stage_used;
+    stage_used += ntiles * tb;
     return b;
   };
   hipStream_t st = n->s_main;
@@ -1510,22 +1599,33 @@ int repartition_impl(nlh_solver *s, const std::vector<int32_t> &own) {
         status = fail(NLH_ERR_HIP, "repartition unpack");
     }
   }
+  tr.mark("enqueue_moves");
   if (hipStreamSynchronize(st) != hipSuccess && status == NLH_OK) status = fail(NLH_ERR_HIP, "repartition sync");
-  for (double *b : bufs) (void)hipFree(b);
+  tr.mark("moves");
+  if (s->stage_cap * sizeof(double) > kStageKeepBytes) {
+    (void)hipFree(s->stage);
+    s->stage = nullptr;
+    s->stage_cap = 0;
+  }
+  tr.mark("free_staging");
   if (status != NLH_OK) {
     const std::string keep = g_err;
     n->comm = nullptr;
+    swap_queues(s, n);  // the old solver's streams back
     destroy_impl(n);
     g_err = keep;
     return status;
   }
+  std::swap(n->stage, s->stage);  // the staging buffer lives on in n
+  std::swap(n->stage_cap, s->stage_cap);
   n->t = s->t;
   n->cur = 0;
   n->halo_fresh = false;
   n->timing = s->timing;
   n->launch_overhead_ms = s->launch_overhead_ms;
   n->pair_overhead_ms = s->pair_overhead_ms;
-  release_impl(s, true);  // the communicator lives on in n
+  release_impl(s, true);  // the communicator lives on in n (and the streams: s holds none now)
+  tr.mark("release_old");
   *s = std::move(*n);
   delete n;  // moved-from shell: its resources now belong to s
   return NLH_OK;

@@ -5,13 +5,16 @@
 #      command, PMC passes and record (tools/bench_evidence.sh) -> gpurun_out/r5v/<workload>/
 #   3. the driver's 20-step C2 line three times, C3 on one block and as 8
 #      virtual ranks, the weak layouts as 2 / 4 / 8 virtual ranks
-#   bash tools/gpu/r5_final.sh COMMIT
+#   bash tools/gpu/r5_final.sh COMMIT [PART]   (PART 1: steps 1 and the 20-step
+#   lines, PART 2: the rest, each within one call's limit; default both)
 set -o pipefail
 export TMPDIR=/tmp
 C=${1:-unknown}
+PART=${2:-all}
 O=gpurun_out/r5z
 E=gpurun_out/r5v
 mkdir -p $O $E
+if [ "$PART" != 2 ]; then
 rm -f gpurun_out/parity_l2.jsonl gpurun_out/parity_nodes.jsonl
 timeout -k 10 1100 python -u -m pytest tests -m gpu -q --maxfail=10 --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc" >> $O/pytest_gpu.log
@@ -21,6 +24,9 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.
 for i in 1 2 3; do
   timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $E/bench20_$i.json 2> $E/bench20_$i.err || exit 1
 done
+echo done > $O/done1
+fi
+[ "$PART" = 1 ] && exit 0
 NLH_N=4096 NLH_EPS=8 tools/bench_evidence.sh $E/c2 k_pair_split weak_4096_eps8_prod 33554432 $C -- || exit 1
 NLH_N=4096 NLH_EPS=8 NLH_TEST=1 tools/bench_evidence.sh $E/test k_pair_split weak_4096_eps8_test 33554432 $C -- --test-mode || exit 1
 NLH_N=8192 NLH_EPS=32 tools/bench_evidence.sh $E/c4 k_wide weak_8192_eps32_prod 67108864 $C -- --eps 32 --lattice 8192 --steps 200 || exit 1
