@@ -64,30 +64,15 @@ __device__ __forceinline__ double rt_wave_prefix(double x) {
 // values) reuse the previous pair's H instead of two more LDS reads and a
 // subtraction -- a uniform (scalar) test per pair
 //
-// CPL: output columns per lane (strips of 64 CPL columns): lane l owns columns
-// l, l + 64, ..; at each offset its CPL prefix values lie 64 apart in LDS, one
-// ds_read2_b64 (offsets 0 and 64, one address add) for two columns with the
-// wave's lanes on consecutive 8-byte words -- no bank conflicts (round 4 had
-// a lane's columns adjacent: 16-byte lane stride, 2.3x slower, profiles/r05/
-// prefix/cpl.jsonl) -- and the staged halo is shared by more columns
+// CPL: output columns per lane (strips of 64 CPL columns); the lane's CPL
+// prefix values at each offset are adjacent in LDS (one ds_read2_b64 for two
+// columns), and the staged halo is shared by more columns
 // PEEL: a full block's first and last R - 1 input rows add only the pairs of
 // the outputs within their horizon (groups of 8 rows)
-// ILV (CPL = 2): the prefix row interleaved with itself shifted by 64,
-// Q[2i] = P_i, Q[2i + 1] = P_{i+64} (P_i = P(i - 1)), so the two columns' values
-// at one offset are one 16-byte ds_read_b128 (256 B/clk, where ds_read2_b64
-// runs at 128) behind one address add: per (pair, column) 1 address add + 2
-// f64 adds instead of 2 + 2.  Each prefix value is written twice.
-template <int NV, int R, bool TEST, bool SKIP = false, bool RUN = false, int CPL = 1, bool PEEL = false,
-          bool ILV = false>
+template <int NV, int R, bool TEST, bool SKIP = false, bool RUN = false, int CPL = 1, bool PEEL = false>
 __global__ __launch_bounds__(64) void k_prefix_rt(RectList L, StepConst C, const int2 *__restrict__ tab) {
-  static_assert(!ILV || CPL == 2, "ILV: two columns per lane");
-  constexpr int QP = 128;           // ILV: front padding of a slot (the shifted copies of P_0 .. P_63)
-  constexpr int NPF = ILV ? QP + 2 * (64 * NV + 1) : 64 * NV + 2;  // doubles per prefix slot
-  // [0] = P(-1) = 0, [1 + k] = P(k); ILV: Q = slot + QP, one slot (a one-wave
-  // workgroup's LDS accesses complete in order: the next row's writes follow
-  // this row's reads), which keeps the larger rows at the LDS of two
-  constexpr int NSLOT = ILV ? 1 : 2;
-  __shared__ __attribute__((aligned(16))) double pf[NSLOT][NPF];
+  constexpr int NPF = 64 * NV + 2;  // doubles per prefix slot: [0] = P(-1) = 0, [1 + k] = P(k)
+  __shared__ __attribute__((aligned(16))) double pf[2][NPF];
   const int lane = (int)threadIdx.x;
   const int E = C.E;
   const int work = xcd_remap(blockIdx.x, gridDim.x);
@@ -99,10 +84,10 @@ __global__ __launch_bounds__(64) void k_prefix_rt(RectList L, StepConst C, const
   const int y0 = Rc.y0 + seg * Rc.seg_rows;
   const int nout = min(R, Rc.y1 - y0);  // seg_rows == R (host)
   const int64_t pitch = Rc.pitch;
-  const int xl = x0 + lane;  // the lane's first column (then + 64 c)
+  const int xl = x0 + CPL * lane;  // the lane's first column
   if (lane == 0) {
-#pragma unroll
-    for (int k = 0; k < NSLOT; ++k) pf[k][ILV ? QP : 0] = 0.0;
+    pf[0][0] = 0.0;
+    pf[1][0] = 0.0;
   }
   // staged window: columns x0 - EP .. x0 - EP + 64 NV - 1 (EP = E rounded up
   // to even: 16-byte aligned rows, each lane's NV values two dwordx4 loads).
@@ -132,7 +117,7 @@ __global__ __launch_bounds__(64) void k_prefix_rt(RectList L, StepConst C, const
   // JLO .. JHI (template constants; pairs past the horizon add +0)
   auto row = [&](int r, auto jlo_c, auto jhi_c) __attribute__((always_inline)) {
     constexpr int JLO = decltype(jlo_c)::value, JHI = decltype(jhi_c)::value;
-    const int s = (r - rfirst) & (NSLOT - 1);
+    const int s = (r - rfirst) & 1;
     if (r + 1 < rend) load_row(r + 1, nxt);
     // prefix row of input row r into slot s
     double p[NV];
@@ -141,34 +126,13 @@ __global__ __launch_bounds__(64) void k_prefix_rt(RectList L, StepConst C, const
     for (int k = 1; k < NV; ++k) p[k] = p[k - 1] + cur[k];
     const double incl = rt_wave_prefix(p[NV - 1]);
     const double ex = incl - p[NV - 1];
-    if constexpr (ILV) {
-      double *q = &pf[s][QP + 2 * (1 + NV * lane)];  // Q[2i], i = 1 + NV lane + k
+    double *dst = &pf[s][1 + NV * lane];
 #pragma unroll
-      for (int k = 0; k < NV; ++k) {
-        q[2 * k] = ex + p[k];
-        q[2 * k - 127] = ex + p[k];  // Q[2 (i - 64) + 1]
-      }
-    } else {
-      double *dst = &pf[s][1 + NV * lane];
-#pragma unroll
-      for (int k = 0; k < NV; ++k) dst[k] = ex + p[k];
-    }
+    for (int k = 0; k < NV; ++k) dst[k] = ex + p[k];
     asm volatile("" ::: "memory");  // LDS is in order per wave: the reads below see every lane's write
     // pairs: output j <- d = r - (y0 + j); table entry d + E + R
     const int2 *t = tab + (r - y0 + E + R);
-    const double *cen = &pf[s][1 + EP + lane];  // the lane's P(c), c = EP + lane (+ 64 per column)
-    const double *cq = &pf[s][QP + 2 * (1 + EP + lane)];  // ILV: Q at the lane's centre
-    auto pair = [&](int j, int2 o) __attribute__((always_inline)) {
-      if constexpr (ILV) {
-        const double2 a = *reinterpret_cast<const double2 *>(cq + 2 * o.x);
-        const double2 b = *reinterpret_cast<const double2 *>(cq + 2 * o.y);
-        acc[j][0] += a.x - b.x;
-        acc[j][CPL - 1] += a.y - b.y;
-      } else {
-#pragma unroll
-        for (int c = 0; c < CPL; ++c) acc[j][c] += cen[o.x + 64 * c] - cen[o.y + 64 * c];
-      }
-    };
+    const double *cen = &pf[s][1 + EP + CPL * lane];  // the lane's P(c), c = EP + CPL lane
     const int jlo = r - y0 - E, jhi = r - y0 + E;  // outputs within this row's horizon
     if constexpr (RUN) {
       double h = 0.0;
@@ -183,12 +147,18 @@ __global__ __launch_bounds__(64) void k_prefix_rt(RectList L, StepConst C, const
     } else if (!SKIP || (jlo <= 0 && jhi >= R - 1)) {
 #pragma unroll
       for (int j = JLO; j <= JHI; ++j) {
-        pair(j, t[-j]);  // t[-j] = {L, -L - 1}, or {0, 0} past the horizon
+        const int2 o = t[-j];  // {L, -L - 1}, or {0, 0} past the horizon
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) acc[j][c] += cen[o.x + c] - cen[o.y + c];
       }
     } else {
 #pragma unroll
       for (int j = 0; j < R; ++j) {
-        if (j >= jlo && j <= jhi) pair(j, t[-j]);
+        if (j >= jlo && j <= jhi) {
+          const int2 o = t[-j];
+#pragma unroll
+          for (int c = 0; c < CPL; ++c) acc[j][c] += cen[o.x + c] - cen[o.y + c];
+        }
       }
     }
     asm volatile("" ::: "memory");
@@ -231,7 +201,7 @@ __global__ __launch_bounds__(64) void k_prefix_rt(RectList L, StepConst C, const
   const double qs = TEST ? C.dt / alpha : 0.0;
 #pragma unroll
   for (int c = 0; c < CPL; ++c) {
-    const int x = xl + 64 * c;
+    const int x = xl + c;
     const bool emit = x < Rc.x1;
     const double sxv = TEST ? C.sxt[Rc.gx0 + min(x, Rc.x1 - 1) + E] : 0.0;
 #pragma unroll

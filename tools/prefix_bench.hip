@@ -73,26 +73,6 @@ int main(int argc, char **argv) {
       {"NV8_R32", k_prefix_rt<8, 32, false>, 32},
       {"NV8_R32_peel", k_prefix_rt<8, 32, false, false, false, 1, true>, 32},
   };
-#elif defined(PX_SET_CPL)
-  // -DPX_SET_CPL: round 5, two output columns per lane (one ds_read2_b64 and
-  // one address add per pair serve both) against the production form
-  std::vector<Variant> vs4 = {
-      {"R32_peel", k_prefix_rt<4, 32, false, false, false, 1, true>, 32},
-      {"R24_cpl2_nv6_peel", k_prefix_rt<6, 24, false, false, false, 2, true>, 24, 2},
-      {"R16_ilv_nv6_peel", k_prefix_rt<6, 16, false, false, false, 2, true, true>, 16, 2},
-      {"R24_ilv_nv6_peel", k_prefix_rt<6, 24, false, false, false, 2, true, true>, 24, 2},
-      {"R32_ilv_nv6_peel", k_prefix_rt<6, 32, false, false, false, 2, true, true>, 32, 2},
-      {"R32_peel_b", k_prefix_rt<4, 32, false, false, false, 1, true>, 32},
-  };
-  std::vector<Variant> vs6 = {
-      {"NV6_R32_peel", k_prefix_rt<6, 32, false, false, false, 1, true>, 32},
-      {"R16_ilv_nv8_peel", k_prefix_rt<8, 16, false, false, false, 2, true, true>, 16, 2},
-      {"R24_ilv_nv8_peel", k_prefix_rt<8, 24, false, false, false, 2, true, true>, 24, 2},
-      {"R32_ilv_nv8_peel", k_prefix_rt<8, 32, false, false, false, 2, true, true>, 32, 2},
-  };
-  std::vector<Variant> vs8 = {
-      {"NV8_R32_peel", k_prefix_rt<8, 32, false, false, false, 1, true>, 32},
-  };
 #else
   std::vector<Variant> vs4 = {
       {"R32", k_prefix_rt<4, 32, false>, 32},
