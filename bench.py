@@ -54,6 +54,23 @@ FP64_LANE_OPS_PEAK = 256 * 64 * 2.4e9  # f64 VALU lane-operations per second (sp
 BYTES_PER_NODE = 16.0          # read u once + write u' once
 
 
+def read_tile_map(path):
+    """The reference's partition file (src/2d_nonlocal_distributed.cpp:476-484):
+    line 1 "nx ny npx npy dh" (tile size, tile counts, spacing), then npx*npy
+    lines "px py owner".  Returns (npx, npy, owner[px + py*npx], tile nx, tile ny)."""
+    import numpy as np
+    tok = open(path).read().split()
+    tnx, tny, npx, npy = (int(v) for v in tok[:4])
+    own = np.full(npx * npy, -1, dtype=np.int32)
+    vals = [int(v) for v in tok[5:5 + 3 * npx * npy]]
+    for i in range(0, len(vals), 3):
+        px, py, o = vals[i:i + 3]
+        own[px + py * npx] = o
+    if (own < 0).any():
+        raise ValueError(f"{path}: not every tile has an owner")
+    return npx, npy, own, tnx, tny
+
+
 def decomposition(n: int):
     """px x py blocks for n ranks: 1x1, 2x1, 2x2, 2x4,
     else px the largest power of two with px^2 <= n dividing n."""
@@ -473,6 +490,11 @@ def main() -> int:
                     help="PXxPY block grid instead of the per-N default (one GPU under NLH_VIRTUAL_RANKS: "
                          "e.g. --strong --lattice 32768 --blocks 2x4 runs C3's 8 ranks on one device)")
     ap.add_argument("--test-mode", action="store_true")
+    # uneven ownership (C5): the reference's --file tile map, tiles resized to
+    # --tile (one GPU runs the owners as NLH_VIRTUAL_RANKS; N > 1 needs one
+    # rank per owner); no CPU baseline / live PMC for this layout
+    ap.add_argument("--map", default="", help="tile -> owner map in the reference's --file format")
+    ap.add_argument("--tile", type=int, default=0, help="tile edge for --map (default: the file's)")
     # J(r) = 1 - r (problem_description.tex:159; not the BASELINE metric, whose J = 1)
     ap.add_argument("--influence", default="constant", choices=["constant", "linear"])
     args = ap.parse_args()
@@ -502,7 +524,7 @@ def _run(args, st: Stages, rank: int, local: int, nranks: int) -> int:
 
     wkey = workload_key(nb, eps, args.strong, args.test_mode) + ("_linear" if args.influence == "linear" else "")
     pmc_live = None
-    if args.pmc == "auto" and args.gpus == 1 and "WORLD_SIZE" not in os.environ:
+    if args.pmc == "auto" and args.gpus == 1 and "WORLD_SIZE" not in os.environ and not args.map:
         pmc_live = live_pmc(args, wkey)  # child processes; this one has not loaded libnlh yet
 
     import nonlocalheatequation_amd as N
@@ -519,11 +541,22 @@ def _run(args, st: Stages, rank: int, local: int, nranks: int) -> int:
             return st.fail(f"process group has {dist.get_world_size()} ranks, expected {args.gpus}", 3)
 
     px, py = decomposition(nranks)
-    if args.blocks:
+    own = None
+    if args.map:
+        px, py, own, tnx, tny = read_tile_map(args.map)
+        if args.tile:
+            tnx = tny = args.tile
+        nowners = int(own.max()) + 1
+        if nranks > 1 and nowners != nranks:
+            return st.fail(f"--map {args.map} has {nowners} owners, the job {nranks} ranks", 2)
+    elif args.blocks:
         px, py = (int(v) for v in args.blocks.lower().split("x"))
         if nranks > 1 and px * py != nranks:
             return st.fail(f"--blocks {args.blocks} needs one block per rank", 2)
-    if args.strong:
+    if own is not None:
+        nx, ny = tnx * px, tny * py
+        nb = nx
+    elif args.strong:
         if nb % px or nb % py:
             return st.fail(f"--lattice {nb} is not divisible by the {px}x{py} block grid", 2)
         nx, ny = nb, nb
@@ -544,8 +577,8 @@ def _run(args, st: Stages, rank: int, local: int, nranks: int) -> int:
     st.enter("nlh_create")  # device, blocks and (N > 1) the RCCL communicator init
     with stdout_to_stderr():
         s = N.Solver(nx, ny, eps, 1.0, dt, dh, test=args.test_mode, kernel=args.kernel, device=local,
-                     rank=rank, nranks=nranks, tiles=(px, py), comm_id=comm_id, seg_rows=args.seg_rows,
-                     influence=args.influence)
+                     rank=rank, nranks=nranks, tiles=(px, py), owner=own, comm_id=comm_id,
+                     seg_rows=args.seg_rows, influence=args.influence)
     info = s.info()
     # every rank owns exactly one block of the px x py grid, and the RCCL
     # communicator itself (ncclCommCount / ncclCommUserRank, nlh_info) must
@@ -698,7 +731,7 @@ def _run(args, st: Stages, rank: int, local: int, nranks: int) -> int:
     result = None
     if rank == 0:
         cpu = None
-        if not args.no_cpu_baseline and nranks == 1 and args.influence == "constant":
+        if not args.no_cpu_baseline and nranks == 1 and args.influence == "constant" and own is None:
             # bounded sample on the workload's own lattice (one step when that
             # fills the budget: C4) and a single-core serial leg
             progress("CPU baseline (bounded sample, after the timed region)")
@@ -714,19 +747,24 @@ def _run(args, st: Stages, rank: int, local: int, nranks: int) -> int:
             "build_id": build_id,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
-            "scaling": "strong" if args.strong else "weak",
+            "scaling": "strong" if args.strong or own is not None else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (test_init IC sin(2 pi x) sin(2 pi y); no dataset)",
             "config": {
-                "workload": workload_name(nb, eps, args.strong, args.test_mode, nx, ny)
+                "workload": workload_name(nb, eps, args.strong or own is not None, args.test_mode, nx, ny)
                             + f", {args.kernel} kernel"
                             + (", J(r) = 1 - r" if args.influence == "linear" else "")
-                            + (f", {px}x{py} blocks + RCCL ghost exchange" if nranks > 1 else ""),
+                            + (f", {px}x{py} blocks + RCCL ghost exchange" if nranks > 1 and own is None else "")
+                            + (f", tile map {os.path.basename(args.map)}: {px}x{py} tiles of {tnx}x{tny}, "
+                               f"{int(own.max()) + 1} owners, RCCL ghost exchange" if own is not None else ""),
                 "lattice": [nx, ny], "eps": eps, "blocks": [px, py], "test_mode": args.test_mode,
                 "disk_points": info.disk_points, "dt": dt, "dh": dh, "kernel": args.kernel,
                 "parallelism": f"{px}x{py} block decomposition, one rank per GPU" if nranks > 1 else "1 GPU",
                 "virtual_ranks": info.owners if nranks == 1 and info.owners > 1 else None,
+                **({"tile_map": os.path.basename(args.map), "tile": [tnx, tny],
+                    "tiles_per_owner": [int(c) for c in __import__("numpy").bincount(own)]}
+                   if own is not None else {}),
             },
             "roofline": {
                 # contract: achieved = ALGORITHMIC bytes (16 B per

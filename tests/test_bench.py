@@ -142,3 +142,20 @@ def test_error_line_rendezvous_timeout():
     assert lines, p.stderr[-2000:]
     rec = json.loads(lines[-1])
     assert rec["rank"] == 1 and rec["stage"] == "process_group", rec
+
+
+def test_read_tile_map_reference_c5():
+    """--map reads the reference's partition files (C5: load_balance_25s_8n,
+    5x5 tiles over 8 owners, 1-7 tiles each)."""
+    path = os.path.join(ROOT, "tests", "golden", "reference_inputs", "load_balance_25s_8n.txt")
+    npx, npy, own, tnx, tny = bench.read_tile_map(path)
+    assert (npx, npy) == (5, 5) and own.shape == (25,) and own.min() == 0 and own.max() == 7
+    counts = [int((own == o).sum()) for o in range(8)]
+    assert sum(counts) == 25 and min(counts) >= 1 and max(counts) <= 7
+    tok = open(path).read().split()
+    assert (tnx, tny) == (int(tok[0]), int(tok[1]))
+    # px outer, as the reference writes it: line i + 1 is tile (px, py) = (i // npy, i % npy)
+    vals = [int(v) for v in tok[5:]]
+    for i in range(25):
+        px, py, o = vals[3 * i:3 * i + 3]
+        assert own[px + py * npx] == o
