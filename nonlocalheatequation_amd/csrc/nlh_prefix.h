@@ -69,11 +69,7 @@ __device__ __forceinline__ double rt_wave_prefix(double x) {
 // columns), and the staged halo is shared by more columns
 // PEEL: a full block's first and last R - 1 input rows add only the pairs of
 // the outputs within their horizon (groups of 8 rows)
-// TPRE: a row's table entries are loaded (scalar) before its prefix scan and
-// waited for before its LDS writes, so no wait on them inside the pair loop
-// drains the LDS reads in flight (scalar and LDS loads share one counter)
-template <int NV, int R, bool TEST, bool SKIP = false, bool RUN = false, int CPL = 1, bool PEEL = false,
-          bool TPRE = false, int BATCH = 0>
+template <int NV, int R, bool TEST, bool SKIP = false, bool RUN = false, int CPL = 1, bool PEEL = false>
 __global__ __launch_bounds__(64) void k_prefix_rt(RectList L, StepConst C, const int2 *__restrict__ tab) {
   constexpr int NPF = 64 * NV + 2;  // doubles per prefix slot: [0] = P(-1) = 0, [1 + k] = P(k)
   __shared__ __attribute__((aligned(16))) double pf[2][NPF];
@@ -122,12 +118,6 @@ __global__ __launch_bounds__(64) void k_prefix_rt(RectList L, StepConst C, const
   auto row = [&](int r, auto jlo_c, auto jhi_c) __attribute__((always_inline)) {
     constexpr int JLO = decltype(jlo_c)::value, JHI = decltype(jhi_c)::value;
     const int s = (r - rfirst) & 1;
-    const int2 *t = tab + (r - y0 + E + R);
-    [[maybe_unused]] int2 tt[TPRE ? JHI - JLO + 1 : 1];
-    if constexpr (TPRE) {
-#pragma unroll
-      for (int j = JLO; j <= JHI; ++j) tt[j - JLO] = t[-j];
-    }
     if (r + 1 < rend) load_row(r + 1, nxt);
     // prefix row of input row r into slot s
     double p[NV];
@@ -136,12 +126,12 @@ __global__ __launch_bounds__(64) void k_prefix_rt(RectList L, StepConst C, const
     for (int k = 1; k < NV; ++k) p[k] = p[k - 1] + cur[k];
     const double incl = rt_wave_prefix(p[NV - 1]);
     const double ex = incl - p[NV - 1];
-    if constexpr (TPRE) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     double *dst = &pf[s][1 + NV * lane];
 #pragma unroll
     for (int k = 0; k < NV; ++k) dst[k] = ex + p[k];
     asm volatile("" ::: "memory");  // LDS is in order per wave: the reads below see every lane's write
     // pairs: output j <- d = r - (y0 + j); table entry d + E + R
+    const int2 *t = tab + (r - y0 + E + R);
     const double *cen = &pf[s][1 + EP + CPL * lane];  // the lane's P(c), c = EP + CPL lane
     const int jlo = r - y0 - E, jhi = r - y0 + E;  // outputs within this row's horizon
     if constexpr (RUN) {
@@ -154,29 +144,10 @@ __global__ __launch_bounds__(64) void k_prefix_rt(RectList L, StepConst C, const
         prev = o;
         acc[j][0] += h;  // (RUN: one column per lane)
       }
-    } else if (BATCH > 0 && !SKIP) {
-      // BATCH: the LDS reads of BATCH pairs first, then their adds
-      constexpr int NB = BATCH > 0 ? BATCH : 1;
-#pragma unroll
-      for (int g = JLO; g <= JHI; g += NB) {
-        double a[NB], b[NB];
-#pragma unroll
-        for (int k = 0; k < NB; ++k)
-          if (g + k <= JHI) {
-            const int2 o = TPRE ? tt[g + k - JLO] : t[-(g + k)];
-            a[k] = cen[o.x];
-            b[k] = cen[o.y];
-          }
-        __builtin_amdgcn_sched_group_barrier(0x100, 2 * NB, 0);  // the DS reads
-        __builtin_amdgcn_sched_group_barrier(0x002, 2 * NB, 0);  // then the VALU
-#pragma unroll
-        for (int k = 0; k < NB; ++k)
-          if (g + k <= JHI) acc[g + k][0] += a[k] - b[k];
-      }
     } else if (!SKIP || (jlo <= 0 && jhi >= R - 1)) {
 #pragma unroll
       for (int j = JLO; j <= JHI; ++j) {
-        const int2 o = TPRE ? tt[j - JLO] : t[-j];  // {L, -L - 1}, or {0, 0} past the horizon
+        const int2 o = t[-j];  // {L, -L - 1}, or {0, 0} past the horizon
 #pragma unroll
         for (int c = 0; c < CPL; ++c) acc[j][c] += cen[o.x + c] - cen[o.y + c];
       }

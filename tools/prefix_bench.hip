@@ -73,28 +73,6 @@ int main(int argc, char **argv) {
       {"NV8_R32", k_prefix_rt<8, 32, false>, 32},
       {"NV8_R32_peel", k_prefix_rt<8, 32, false, false, false, 1, true>, 32},
   };
-#elif defined(PX_SET_TB)
-  // -DPX_SET_TB: round 5, the row's table entries loaded before its scan
-  // (TPRE) and the LDS reads of BATCH pairs issued before their adds
-  std::vector<Variant> vs4 = {
-      {"R32_peel", k_prefix_rt<4, 32, false, false, false, 1, true>, 32},
-      {"R32_peel_tpre", k_prefix_rt<4, 32, false, false, false, 1, true, true>, 32},
-      {"R32_peel_b8", k_prefix_rt<4, 32, false, false, false, 1, true, false, 8>, 32},
-      {"R32_peel_tpre_b8", k_prefix_rt<4, 32, false, false, false, 1, true, true, 8>, 32},
-      {"R32_peel_tpre_b16", k_prefix_rt<4, 32, false, false, false, 1, true, true, 16>, 32},
-      {"R32_peel_tpre_b4", k_prefix_rt<4, 32, false, false, false, 1, true, true, 4>, 32},
-      {"R32_peel_again", k_prefix_rt<4, 32, false, false, false, 1, true>, 32},
-  };
-  std::vector<Variant> vs6 = {
-      {"NV6_R32_peel", k_prefix_rt<6, 32, false, false, false, 1, true>, 32},
-      {"NV6_R32_peel_tpre_b8", k_prefix_rt<6, 32, false, false, false, 1, true, true, 8>, 32},
-      {"NV6_R32_peel_b8", k_prefix_rt<6, 32, false, false, false, 1, true, false, 8>, 32},
-  };
-  std::vector<Variant> vs8 = {
-      {"NV8_R32_peel", k_prefix_rt<8, 32, false, false, false, 1, true>, 32},
-      {"NV8_R32_peel_tpre_b8", k_prefix_rt<8, 32, false, false, false, 1, true, true, 8>, 32},
-      {"NV8_R32_peel_b8", k_prefix_rt<8, 32, false, false, false, 1, true, false, 8>, 32},
-  };
 #else
   std::vector<Variant> vs4 = {
       {"R32", k_prefix_rt<4, 32, false>, 32},
