@@ -232,3 +232,23 @@ def test_long_run_two_step_pass_vs_oracle(oracle):
     ref = oracle.run(oracle.params(nx, ny, eps, 1.0, dt, dh, 0), nt, u0)
     scale = np.max(np.abs(ref))
     check_nodes(u, ref, scale=scale)
+
+
+def test_bench_line_uneven_tile_map():
+    """bench.py --map: the reference's uneven map (load_balance_25s_8n) as 8
+    virtual owners on this GPU, small tiles -- the line names the map, the
+    owners' tile counts and carries the exchange report."""
+    import subprocess
+    import sys
+    m = os.path.join(ROOT, "tests", "golden", "reference_inputs", "load_balance_25s_8n.txt")
+    env = dict(os.environ, NLH_VIRTUAL_RANKS="8")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--map", m, "--tile", "512",
+                          "--steps", "4", "--warmup", "2", "--warmup-ms", "0", "--pmc", "off",
+                          "--no-cpu-baseline", "--phase-passes", "4"],
+                         capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-2000:]
+    line = json.loads(out.stdout.strip().splitlines()[-1])
+    c = line["config"]
+    assert c["lattice"] == [2560, 2560] and c["tile_map"] == "load_balance_25s_8n.txt"
+    assert c["virtual_ranks"] == 8 and sum(c["tiles_per_owner"]) == 25 and min(c["tiles_per_owner"]) >= 1
+    assert line["value"] > 0 and line["scaling"] == "strong" and line["exchange"]["passes_timed"] > 0
