@@ -705,10 +705,6 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
         const int i = b + q;
         if constexpr ((ABL & 32) == 0 && !RB::LEAN)
           if (i > i_last) return;
-        // OPT & 8192 / 16384 (harness): wave 1 at priority 3 for its DMA and
-        // window reads only, then 1 / 0 (both: 2) for its math and store
-        constexpr int PLOW = (OPT & 24576) == 24576 ? 2 : (OPT & 16384) ? 0 : 1;
-        if constexpr ((OPT & 24576) != 0) __builtin_amdgcn_s_setprio(3);
         issue(kslot(bs, q + DT));  // u^t row i+DT (clamped; never a slot wave 0 still reads)
         // u^{t+1} row m2 = i - 2E - B (m2 mod P == q2); rows m2 < 0 are LDS
         // garbage that only reaches accumulators of rows never emitted, each
@@ -718,7 +714,6 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
         double (&w2)[NW] = wr[q & 1];
         if constexpr (!PF || (q & 1) == 0) window(u1buf + uslot(m2, q - 2 * E - B) * U1W + R * lane, w2);
         if constexpr (PF && (q & 1) == 0) window(u1buf + uslot(m2 + 1, q + 1 - 2 * E - B) * U1W + R * lane, wr[1]);
-        if constexpr ((OPT & 24576) != 0) __builtin_amdgcn_s_setprio(PLOW);
         if constexpr (PI) {
           static_assert((q2 & 1) == (q & 1), "row pairs follow the barrier blocks");
           if constexpr ((q & 1) == 0)

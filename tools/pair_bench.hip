@@ -218,15 +218,6 @@ int main(int argc, char **argv) {
       {"opt2063", k_pair_split<E, 4, 0, 2, false, 2063>, 128, 4, 128 - 2 * E},
       {"opt6623", k_pair_split<E, 4, 0, 2, false, 6623>, 128, 4, 128 - 2 * E},
   };
-#elif defined(PB_SET_PRIO2)
-  // -DPB_SET_PRIO2: wave 1 at priority 3 only for its DMA + window reads, then
-  // 1 (8192), 0 (16384) or 2 (24576) for its math, against the fixed priority
-  std::vector<Variant> vs = {
-      {"opt6623", k_pair_split<E, 4, 0, 2, false, 6623>, 128, 4, 128 - 2 * E},
-      {"opt14815", k_pair_split<E, 4, 0, 2, false, 6623 | 8192>, 128, 4, 128 - 2 * E},
-      {"opt23007", k_pair_split<E, 4, 0, 2, false, 6623 | 16384>, 128, 4, 128 - 2 * E},
-      {"opt31199", k_pair_split<E, 4, 0, 2, false, 6623 | 24576>, 128, 4, 128 - 2 * E},
-  };
 #elif defined(PB_SET_BIG)
   // -DPB_SET_BIG: the multi-round regime (16384^2 / 32768^2 as one block, the
   // host launches without the wave priority): round-4 NP (7) against the
