@@ -171,8 +171,8 @@ constexpr EnvKnob kEnvKnobs[] = {
     {"NLH_BAND_SEG", 0, 1 << 20},  // edge-band segment height (0 = automatic)
     {"NLH_COMM_INIT_TIMEOUT", 1, 86400},  // seconds a communicator init may take (default 300)
     {"NLH_SYNC", 0, 3},            // host waits: 0 spin (default), 1 yield, 2 blocking, 3 HIP's auto
-    {"NLH_PAIR_PRIO", 0, 2},
-    {"NLH_TRACE_REPART", 0, 1},    // repartition phase times on stderr       // k_pair_split wave priority: 0 never, 1 one-round lists, 2 and not on bands
+    {"NLH_PAIR_PRIO", 0, 2},       // k_pair_split wave priority: 0 never, 1 one-round lists (default), 2 not on bands
+    {"NLH_TRACE_REPART", 0, 1},    // repartition phase times on stderr
 };
 constexpr const char *kRemovedKnobs[] = {"NLH_ABLATE", "NLH_PAIR_ABLATE"};
 
