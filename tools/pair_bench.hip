@@ -218,6 +218,11 @@ int main(int argc, char **argv) {
       {"opt2063", k_pair_split<E, 4, 0, 2, false, 2063>, 128, 4, 128 - 2 * E},
       {"opt6623", k_pair_split<E, 4, 0, 2, false, 6623>, 128, 4, 128 - 2 * E},
   };
+#elif defined(PB_SET_ONE)
+  // -DPB_SET_ONE: the production pass alone (compiler-option A/B: one binary per option)
+  std::vector<Variant> vs = {
+      {PB_NAME, k_pair_split<E, 4, 0, 2, false, 6623>, 128, 4, 128 - 2 * E},
+  };
 #elif defined(PB_SET_BIG)
   // -DPB_SET_BIG: the multi-round regime (16384^2 / 32768^2 as one block, the
   // host launches without the wave priority): round-4 NP (7) against the
