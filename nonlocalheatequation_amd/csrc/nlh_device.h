@@ -66,14 +66,6 @@ struct StepConst {
   double jsum;
   double st2pi2;   // st2pi, ct at time t+1 (two-step test mode: the second step's source)
   double ct2;
-  // separable L_h[W0] (two-step test mode, nlh_pair.h OPT & 32768):
-  // L_h[W0](x, y) = cdh2 (sum_l Sx'_l(x) Ty_l(y) + sx(x) Z(y)); lsx rows
-  // l < NLV: Sx'_l, row NLV: sx (0 outside the lattice), over global columns
-  // -2E .. (stride pair_sep_ncol); lty rows y = -2E .. ny+2E-1 (stride
-  // pair_sep_stride(E)): Ty_l(y) for l < NLV, Z(y) at NLV
-  const double *lsx;
-  const double *lty;
-  double cdh2;     // c2d * dh2
 };
 
 // Strided rectangle copy (halo exchange: local block->block copies, pack to

@@ -87,35 +87,6 @@ __host__ __device__ constexpr int pair_opt(int E) {
                 : (E == 13 ? 14 | 16 : (E <= 12 && pair_rows(E) ? 15 | 16 | 64 : 15 | 16));
 }
 
-// separable L_h[W0] (OPT & 32768): the distinct half-widths L > 0 of the disk
-// rows in order of first appearance (d = 0, 1, ..), their count NLV, and the
-// row stride of the per-row table (NLV values + Z, a power of two)
-__host__ __device__ constexpr int pair_sep_level(int E, int l) {
-  int k = 0, prev = -1;
-  for (int d = 0; d <= E; ++d) {
-    const int L = clen(E, d);
-    if (L > 0 && L != prev) {
-      if (k == l) return L;
-      ++k;
-    }
-    prev = L;
-  }
-  return -1;
-}
-__host__ __device__ constexpr int pair_sep_nlv(int E) {
-  int n = 0;
-  while (pair_sep_level(E, n) > 0) ++n;
-  return n;
-}
-// columns of the per-column table: global -2E .. nx + 2E + 127 (a last strip's
-// stage-1 columns reach past the lattice; 0 there)
-__host__ __device__ constexpr int64_t pair_sep_ncol(int E, int64_t nx) { return nx + 4 * E + 128; }
-__host__ __device__ constexpr int pair_sep_stride(int E) {
-  int s = 1;
-  while (s < pair_sep_nlv(E) + 1) s *= 2;
-  return s;
-}
-
 // some row offset d of the disk has half-width len(d) == L
 __host__ __device__ constexpr bool pair_level_used(int E, int L) {
   for (int d = 0; d <= E; ++d)
@@ -419,11 +390,7 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
   constexpr int LOFF = E & 1;
   constexpr int NCHL = TEST ? (W1 + LOFF + 1) / 2 : 0;
   constexpr int LWW = 2 * NCHL;
-  // OPT & 32768 (test mode): L_h[W0] rows computed by wave 1 from the
-  // separable tables (StepConst lsx / lty) instead of read from HBM
-  constexpr bool SEP = TEST && (OPT & 32768) != 0;
-  constexpr int NLV = SEP ? pair_sep_nlv(E) : 0;
-  constexpr int GT = TEST ? (SEP ? 0 : (NCHL + 63) / 64) + 1 : 0;  // + the sin(2 pi y dh) pair
+  constexpr int GT = TEST ? (NCHL + 63) / 64 + 1 : 0;  // + the sin(2 pi y dh) pair
   constexpr int GA = G + GT;            // DMA instructions per row
   static_assert((B & (B - 1)) == 0, "B must be a power of two");
   static_assert(D * GA + D + 1 < 64, "vmcnt range");
@@ -664,43 +631,13 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
     const double *lw0p = TEST ? Rc.lw + (x0 - E - LOFF) : nullptr;
     const uint32_t llw = __builtin_amdgcn_readfirstlane(lds_addr(lwr));
     const uint32_t lsy = __builtin_amdgcn_readfirstlane(lds_addr(syr));
-    // SEP: the lane's two stage-1 columns' Sx'_l and sx, for the whole segment
-    [[maybe_unused]] double sxp[NLV + 1][R];
-    if constexpr (SEP) {
-      const int64_t ncol = pair_sep_ncol(E, C.nx);
-      const double *t = C.lsx + (rgx0 + x0 - E + R * lane + 2 * E);
-#pragma unroll
-      for (int l = 0; l <= NLV; ++l)
-#pragma unroll
-        for (int c = 0; c < R; ++c) sxp[l][c] = t[l * ncol + c];
-    }
     auto issue = [&](int slot) {
       if constexpr (TEST) {
         // L_h[W0] and sin(2 pi y dh) of u^{t+1} row irow - 2E (stage 1's output
         // when it reads u^t row irow)
         const int m = irow - 2 * E;
-        if constexpr (SEP) {
-          // L_h[W0] of that row from the separable tables, into the ring slot
-          // the DMA would fill (the block-end barrier orders it before wave 0)
-          const double *ty = C.lty + (int64_t)(rgy0 + m_row(m) + 2 * E) * pair_sep_stride(E);
-          double a[R];
-#pragma unroll
-          for (int c = 0; c < R; ++c) {
-            a[c] = sxp[NLV][c] * ty[NLV];
-#pragma unroll
-            for (int l = 0; l < NLV; ++l) a[c] = fma(sxp[l][c], ty[l], a[c]);
-          }
-          double *dl = lwr + slot * LWW + LOFF + R * lane;
-          if constexpr (LOFF == 0) {
-            *reinterpret_cast<double2 *>(dl) = make_double2(C.cdh2 * a[0], C.cdh2 * a[1]);
-          } else {
-            dl[0] = C.cdh2 * a[0];
-            dl[1] = C.cdh2 * a[1];
-          }
-        }
         if (!(ABL & 2) && !(ABL & 256)) {
-          if constexpr ((ABL & 16384) == 0 && !SEP)  // ablation 16384: no L_h[W0] row DMA
-            dma_chunks<NCHL, false, false>(lw0p + (int64_t)m_row(m) * pitch, llw + slot * LWW * 8, lane);
+          dma_chunks<NCHL, false, false>(lw0p + (int64_t)m_row(m) * pitch, llw + slot * LWW * 8, lane);
           dma_chunks<1, false, false>(C.syt + (sy_idx(m) & ~1), lsy + slot * 16, lane);
         }
         ++irow;
