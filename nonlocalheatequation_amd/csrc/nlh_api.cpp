@@ -277,6 +277,7 @@ struct nlh_solver {
   bool weighted = false;  // k_weighted: non-constant influence function
   bool prefix = false;    // k_prefix_rt (nlh_prefix.h) past the k_wide horizons
   int32_t *d_ptab = nullptr;  // k_prefix_rt's per-offset prefix index table
+  double *d_lsx = nullptr, *d_lty = nullptr;  // two-step test mode: separable L_h[W0] tables (sep_tables)
   double *d_wt = nullptr, *d_qj = nullptr;  // J tables (influence != 0)
   int halo = 0;       // halo rows/columns held per block: eps, or 2*eps with pair
   // production k_pair_split rings: 6 = D4/B2 (default; with row pairs 444-450 vs 438-446 G
@@ -999,6 +1000,8 @@ void release_impl(nlh_solver *s, bool keep_comm) {
   (void)hipFree(s->d_wt);
   (void)hipFree(s->d_qj);
   (void)hipFree(s->d_ptab);
+  (void)hipFree(s->d_lsx);
+  (void)hipFree(s->d_lty);
   (void)hipFree(s->d_sxt);
   (void)hipFree(s->d_syt);
   (void)hipFree(s->d_lens);
@@ -1034,6 +1037,63 @@ void swap_queues(nlh_solver *a, nlh_solver *b) {
   std::swap(a->ev_band, b->ev_band);
   std::swap(a->ev_int, b->ev_int);
   std::swap(a->ev_pool, b->ev_pool);
+}
+
+// The two-step test-mode pass's separable L_h[W0] (nlh_pair.h OPT & 32768).
+// With the reference's zero-extended W0 = sx(x) sy(y) (sx, sy the glibc sin
+// values, 0 outside the lattice; sum_local_test, src/2d_nonlocal_serial.cpp:
+// 235-252) and the disk as rows dy of half-width len(|dy|):
+//   L_h[W0](x, y) = c dh^2 (sum_dy sy(y+dy) Sx_len(|dy|)(x) - N sx(x) sy(y))
+//                 = c dh^2 (sum_l Sx'_l(x) Ty_l(y) + sx(x) Z(y)),
+// Sx_L = sum_{|dx| <= L} sx(x+dx), Sx'_L = Sx_L - (2L+1) sx (small: no
+// cancellation left), Ty_l = the sum of sy(y+dy) over the rows of level l,
+// Z = sum_dy (2 len(|dy|) + 1) sy(y+dy) - N sy(y); levels l: the distinct
+// len > 0 in order of d (L = 0 rows only enter Z).  Long double sums, c dh^2
+// folded into lsx.
+int sep_tables(nlh_solver *s, const std::vector<int32_t> &lens) {
+  const nlh_params &p = s->p;
+  const int E = (int)p.eps;
+  std::vector<int> lev;  // = nlh_pair.h pair_sep_level(E, l)
+  for (int d = 0, prev = -1; d <= E; ++d) {
+    if (lens[d] > 0 && lens[d] != prev) lev.push_back(lens[d]);
+    prev = lens[d];
+  }
+  const int nlv = (int)lev.size(), lts = nlh::pair_sep_stride_n(nlv);
+  const int64_t ncol = nlh::pair_sep_ncol(E, p.nx);
+  auto sx = [&](int64_t g) -> long double { return (g >= 0 && g < p.nx) ? (long double)sin(2 * M_PI * (g * p.dh)) : 0.0L; };
+  auto sy = [&](int64_t g) -> long double { return (g >= 0 && g < p.ny) ? (long double)sin(2 * M_PI * (g * p.dh)) : 0.0L; };
+  const long double cd = (long double)s->sc.c2d * (long double)s->sc.dh2;
+  std::vector<double> lsx((size_t)(nlv + 1) * ncol, 0.0), lty((size_t)(p.ny + 4 * E) * lts, 0.0);
+  for (int64_t c = 0; c < ncol; ++c) {
+    const int64_t g = c - 2 * E;
+    if (g < 0 || g >= p.nx) continue;
+    for (int l = 0; l < nlv; ++l) {
+      long double sum = 0.0L;
+      for (int dx = -lev[l]; dx <= lev[l]; ++dx) sum += sx(g + dx);
+      lsx[(size_t)l * ncol + c] = (double)(cd * (sum - (2 * lev[l] + 1) * sx(g)));
+    }
+    lsx[(size_t)nlv * ncol + c] = (double)(cd * sx(g));
+  }
+  for (int64_t r = 0; r < p.ny + 4 * E; ++r) {
+    const int64_t y = r - 2 * E;
+    if (y < 0 || y >= p.ny) continue;
+    long double z = -(long double)s->disk * sy(y);
+    for (int d = -E; d <= E; ++d) z += (2 * lens[d < 0 ? -d : d] + 1) * sy(y + d);
+    for (int l = 0; l < nlv; ++l) {
+      long double sum = 0.0L;
+      for (int d = -E; d <= E; ++d)
+        if (lens[d < 0 ? -d : d] == lev[l]) sum += sy(y + d);
+      lty[(size_t)r * lts + l] = (double)sum;
+    }
+    lty[(size_t)r * lts + nlv] = (double)z;
+  }
+  HIP_TRY(hipMalloc(&s->d_lsx, lsx.size() * sizeof(double)));
+  HIP_TRY(hipMalloc(&s->d_lty, lty.size() * sizeof(double)));
+  HIP_TRY(hipMemcpy(s->d_lsx, lsx.data(), lsx.size() * sizeof(double), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(s->d_lty, lty.data(), lty.size() * sizeof(double), hipMemcpyHostToDevice));
+  s->sc.lsx = s->d_lsx;
+  s->sc.lty = s->d_lty;
+  return NLH_OK;
 }
 
 // reuse_comm: an existing communicator over the same ranks (nlh_repartition);
@@ -1204,6 +1264,10 @@ int create_impl(const nlh_params *pin, nlh_solver *s, ncclComm_t reuse_comm = nu
     nlh::prefix_rt_table(E, lens.data(), tab.data());
     HIP_TRY(hipMalloc(&s->d_ptab, tab.size() * sizeof(int32_t)));
     HIP_TRY(hipMemcpy(s->d_ptab, tab.data(), tab.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+  }
+  if (s->pair && p.test) {
+    int rc2 = sep_tables(s, lens);
+    if (rc2) return rc2;
   }
   s->sc.sxt = s->d_sxt;
   s->sc.syt = s->d_syt;

@@ -66,6 +66,14 @@ struct StepConst {
   double jsum;
   double st2pi2;   // st2pi, ct at time t+1 (two-step test mode: the second step's source)
   double ct2;
+  // separable L_h[W0] (two-step test mode, nlh_pair.h OPT & 32768):
+  // L_h[W0](x, y) = sum_l Sx'_l(x) Ty_l(y) + sx(x) Z(y), c dh^2 folded into
+  // lsx; lsx rows l < NLV: Sx'_l, row NLV: sx (0 outside the lattice), over
+  // global columns -2E .. (stride pair_sep_ncol); lty rows y = -2E ..
+  // ny+2E-1 (stride pair_sep_stride(E)): Ty_l(y) for l < NLV, Z(y) at NLV
+  // (nlh_api.cpp sep_tables)
+  const double *lsx;
+  const double *lty;
 };
 
 // Strided rectangle copy (halo exchange: local block->block copies, pack to
@@ -110,6 +118,17 @@ int pair_strip_width(int E);  // output columns per strip: 128 - 2E
 int pair_blocks_per_cu(int E, int variant);  // resident workgroups per CU (0 = unknown)
 // or'ed into variant 5 / 6: the same kernel without the wave priority (nlh_pair.h)
 constexpr int kPairNoPrio = 0x100;
+
+// separable L_h[W0] tables (StepConst lsx / lty; nlh_pair.h OPT & 32768):
+// columns of lsx -- global -2E .. nx + 2E + 127 (a last strip's stage-1
+// columns reach past the lattice; 0 there) -- and the lty row stride for nlv
+// levels (nlv values + Z, a power of two)
+constexpr int64_t pair_sep_ncol(int E, int64_t nx) { return nx + 4 * E + 128; }
+constexpr int pair_sep_stride_n(int nlv) {
+  int s = 1;
+  while (s < nlv + 1) s *= 2;
+  return s;
+}
 int launch_pair(const RectList &rl, const StepConst &c, int variant, void *stream);
 int launch_exact(const RectList &rl, const StepConst &c, bool test, void *stream);
 // fast path for a non-constant J (influence != 0, eps <= 32): LDS tile of

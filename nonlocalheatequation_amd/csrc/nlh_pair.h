@@ -79,13 +79,40 @@ constexpr int kPairSplitB = 4;  // k_pair_split: rows per barrier
 // rings whose slot counts divide the period (production; E = 8: 27.7 KB of
 // LDS per workgroup, 4 per CU): 67.62 -> 66.44 us (profiles/r05/pair/ring_*).
 // 512 (harness only) puts wave 0 at the wave priority instead of wave 1;
-// 1024 (harness only) the lean stage 2 (spills).
+// 1024 (harness only) the lean stage 2 (spills).  32768 (test mode, E = 8):
+// the L_h[W0] rows from the separable form L_h[W0] = sum_l Sx'_l(x) Ty_l(y)
+// + sx(x) Z(y) (StepConst lsx / lty) -- per row a 64-byte Ty / Z DMA instead
+// of the 1-KB L_h[W0] row, wave 1 forming the row B iterations ahead of wave
+// 0: C2 test-mode harness 98.9 -> 94.7 us per pass, 4.4e-16 from the field
+// (profiles/r05/pair/test_sep2_reps4.jsonl; the row DMA itself costs 15%).
 constexpr int kPairPadRows = 16;
 __host__ __device__ constexpr bool pair_rows(int E);
 __host__ __device__ constexpr int pair_opt(int E) {
-  return E == 8 ? 15 | 16 | 64 | 128 | 256 | 2048 | 4096
+  return E == 8 ? 15 | 16 | 64 | 128 | 256 | 2048 | 4096 | 32768
                 : (E == 13 ? 14 | 16 : (E <= 12 && pair_rows(E) ? 15 | 16 | 64 : 15 | 16));
 }
+
+// separable L_h[W0] (OPT & 32768): the distinct half-widths L > 0 of the disk
+// rows in order of first appearance (d = 0, 1, ..), their count NLV, and the
+// row stride of the per-row table (NLV values + Z, a power of two)
+__host__ __device__ constexpr int pair_sep_level(int E, int l) {
+  int k = 0, prev = -1;
+  for (int d = 0; d <= E; ++d) {
+    const int L = clen(E, d);
+    if (L > 0 && L != prev) {
+      if (k == l) return L;
+      ++k;
+    }
+    prev = L;
+  }
+  return -1;
+}
+__host__ __device__ constexpr int pair_sep_nlv(int E) {
+  int n = 0;
+  while (pair_sep_level(E, n) > 0) ++n;
+  return n;
+}
+__host__ __device__ constexpr int pair_sep_stride(int E) { return pair_sep_stride_n(pair_sep_nlv(E)); }
 
 // some row offset d of the disk has half-width len(d) == L
 __host__ __device__ constexpr bool pair_level_used(int E, int L) {
@@ -338,7 +365,8 @@ __host__ __device__ constexpr int pair_tail_len(int E, int c) {
 // 4 = windows from registers (no LDS window reads), 8 = no s_barrier,
 // 16 = no u^{t+1} LDS writes, 32 = no per-row range checks (rows past the
 // segment end computed too), 64 = no vmcnt waits for the DMA'd rows, 128 = no
-// output stores, 256 = no DMA, 512 = non-temporal stores, 1024 = non-temporal DMA
+// output stores, 256 = no DMA, 512 = non-temporal stores, 1024 = non-temporal DMA,
+// 16384 = (test mode) no L_h[W0] row DMA
 
 // k_pair_split: the two stages of k_pair on the two waves of one workgroup,
 // synchronised once per block of B rows (s_barrier):
@@ -390,7 +418,13 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
   constexpr int LOFF = E & 1;
   constexpr int NCHL = TEST ? (W1 + LOFF + 1) / 2 : 0;
   constexpr int LWW = 2 * NCHL;
-  constexpr int GT = TEST ? (NCHL + 63) / 64 + 1 : 0;  // + the sin(2 pi y dh) pair
+  // OPT & 32768 (test mode): L_h[W0] rows formed by wave 1 from the
+  // separable tables (StepConst lsx / lty) instead of read from HBM
+  constexpr bool SEP = TEST && (OPT & 32768) != 0;
+  constexpr int NLV = SEP ? pair_sep_nlv(E) : 0;
+  constexpr int LTS = SEP ? pair_sep_stride(E) : 0;
+  // SEP: one DMA per row for the row's Ty / Z values (LTS doubles) instead of its L_h[W0] row
+  constexpr int GT = TEST ? (SEP ? 1 : (NCHL + 63) / 64) + 1 : 0;  // + the sin(2 pi y dh) pair
   constexpr int GA = G + GT;            // DMA instructions per row
   static_assert((B & (B - 1)) == 0, "B must be a power of two");
   static_assert(D * GA + D + 1 < 64, "vmcnt range");
@@ -398,11 +432,13 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
   static_assert(P <= 2 * E + B, "the peeled iterations 0 .. P-1 carry no u^{t+1} row");
   static_assert((OPT & 2) == 0 || 2 * B + D <= kPairPadRows, "tail DMAs past the padding rows");
 
-  __shared__ __attribute__((aligned(16))) double ring[K * RW + U1R * U1W + (TEST ? U1R * U1W + K * LWW + 2 * K : 0)];
+  __shared__ __attribute__((aligned(16))) double ring[K * RW + U1R * U1W + (TEST ? U1R * U1W + K * LWW + 2 * K : 0) +
+                                                     K * LTS];
   double *const u1buf = ring + K * RW;
   double *const qbuf = u1buf + U1R * U1W;  // TEST: (dt/alpha) b(t+1) of the u^{t+1} rows
   double *const lwr = qbuf + U1R * U1W;    // TEST: L_h[W0] rows, slots of the u^t ring
   double *const syr = lwr + K * LWW;       // TEST: sin(2 pi y dh) pairs, same slots
+  [[maybe_unused]] double *const tyr = syr + 2 * K;  // SEP: Ty / Z rows, same slots
   // ring slots: bsv = b mod K (0 with RP), q = the row's place in the period
   auto kslot = [](int bsv, int q) __attribute__((always_inline)) { return RP ? q % K : (bsv + q) & (K - 1); };
   auto uslot = [](int m, int qm) __attribute__((always_inline)) {
@@ -631,13 +667,53 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
     const double *lw0p = TEST ? Rc.lw + (x0 - E - LOFF) : nullptr;
     const uint32_t llw = __builtin_amdgcn_readfirstlane(lds_addr(lwr));
     const uint32_t lsy = __builtin_amdgcn_readfirstlane(lds_addr(syr));
+    // SEP: the lane's two stage-1 columns' Sx'_l and sx, for the whole segment
+    [[maybe_unused]] double sxp[NLV + 1][R];
+    if constexpr (SEP) {
+      const int64_t ncol = pair_sep_ncol(E, C.nx);
+      const double *t = C.lsx + (rgx0 + x0 - E + R * lane + 2 * E);
+#pragma unroll
+      for (int l = 0; l <= NLV; ++l)
+#pragma unroll
+        for (int c = 0; c < R; ++c) sxp[l][c] = t[l * ncol + c];
+    }
+    [[maybe_unused]] const uint32_t ltyr = __builtin_amdgcn_readfirstlane(lds_addr(tyr));
+    // SEP: L_h[W0] of the row in ring slot `slot` from its DMA'd Ty / Z row
+    // (uniform LDS reads) and the lane's Sx' (registers; the host folds c dh^2
+    // into them), into the slot wave 0 reads
+    auto lw_compute = [&](int slot) __attribute__((always_inline)) {
+      if constexpr (SEP) {
+        const double *ty = tyr + slot * LTS;
+        double a[R];
+#pragma unroll
+        for (int c = 0; c < R; ++c) {
+          a[c] = sxp[NLV][c] * ty[NLV];
+#pragma unroll
+          for (int l = 0; l < NLV; ++l) a[c] = fma(sxp[l][c], ty[l], a[c]);
+        }
+        double *dl = lwr + slot * LWW + LOFF + R * lane;
+        if constexpr (LOFF == 0) {
+          *reinterpret_cast<double2 *>(dl) = make_double2(a[0], a[1]);
+        } else {
+          dl[0] = a[0];
+          dl[1] = a[1];
+        }
+      }
+    };
     auto issue = [&](int slot) {
       if constexpr (TEST) {
         // L_h[W0] and sin(2 pi y dh) of u^{t+1} row irow - 2E (stage 1's output
         // when it reads u^t row irow)
         const int m = irow - 2 * E;
         if (!(ABL & 2) && !(ABL & 256)) {
-          dma_chunks<NCHL, false, false>(lw0p + (int64_t)m_row(m) * pitch, llw + slot * LWW * 8, lane);
+          // SEP: the Ty / Z row of u^t row irow + B (its L_h[W0] row is
+          // computed by lw_compute at wave 1's iteration irow - DT, B rows
+          // ahead of wave 0: landed by then, and never in the block wave 0 holds)
+          if constexpr (SEP)
+            dma_chunks<LTS / 2, false, false>(C.lty + (int64_t)(rgy0 + m_row(m + B) + 2 * E) * LTS,
+                                              ltyr + ((slot + B) & (K - 1)) * LTS * 8, lane);
+          if constexpr ((ABL & 16384) == 0 && !SEP)  // ablation 16384: no L_h[W0] row DMA
+            dma_chunks<NCHL, false, false>(lw0p + (int64_t)m_row(m) * pitch, llw + slot * LWW * 8, lane);
           dma_chunks<1, false, false>(C.syt + (sy_idx(m) & ~1), lsy + slot * 16, lane);
         }
         ++irow;
@@ -654,9 +730,18 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
       else if (++row < n_in)
         gnext += stride;
     };
+    if constexpr (SEP) {  // the Ty / Z rows of u^t rows 0 .. B-1 (the issues below carry rows B ..)
+#pragma unroll
+      for (int r = 0; r < B; ++r)
+        dma_chunks<LTS / 2, false, false>(C.lty + (int64_t)(rgy0 + m_row(r - 2 * E) + 2 * E) * LTS,
+                                          ltyr + r * LTS * 8, lane);
+    }
 #pragma unroll
     for (int s = 0; s < DT; ++s) issue(s);
     wait_vmcnt<D * GA>();  // rows 0 .. B-1 landed (D rows may still fly)
+    if constexpr (SEP)
+#pragma unroll
+      for (int r = 0; r < B; ++r) lw_compute(r);
     row_barrier();
     const int xo = x0 + R * lane;
     const bool emit0 = R * lane < WO && xo < rx1;
@@ -689,6 +774,7 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
     // branch (a conditional scatter makes the compiler copy them around)
     for (int i = 0; i < P; ++i) {
       issue(RP ? (i + DT < K ? i + DT : i + DT - K) : (i + DT) & (K - 1));
+      lw_compute((i + B) & (K - 1));  // SEP: the L_h[W0] row of u^t row i + B
       block_end(i);
     }
     int bs = P & (K - 1);  // b % K
@@ -706,6 +792,7 @@ __global__ __launch_bounds__(128, 2) void k_pair_split(RectList L, StepConst C) 
         if constexpr ((ABL & 32) == 0 && !RB::LEAN)
           if (i > i_last) return;
         issue(kslot(bs, q + DT));  // u^t row i+DT (clamped; never a slot wave 0 still reads)
+        lw_compute(kslot(bs, q + B));  // SEP: the L_h[W0] row of u^t row i + B
         // u^{t+1} row m2 = i - 2E - B (m2 mod P == q2); rows m2 < 0 are LDS
         // garbage that only reaches accumulators of rows never emitted, each
         // assigned afresh before use

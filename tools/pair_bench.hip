@@ -223,6 +223,17 @@ int main(int argc, char **argv) {
   std::vector<Variant> vs = {
       {PB_NAME, k_pair_split<E, 4, 0, 2, false, 6623>, 128, 4, 128 - 2 * E},
   };
+#elif defined(PB_SET_TESTABL)
+  // -DPB_SET_TESTABL: the test-mode pass with and without its L_h[W0] row DMA
+  // (ablation 16384; results not meaningful), with the separable L_h[W0]
+  // (OPT 32768: the library's E = 8 default from round 5), beside the
+  // production pass
+  std::vector<Variant> vs = {
+      {"test", k_pair_split<E, 4, 0, 2, true, 6623>, 128, 4, 128 - 2 * E},
+      {"test_nolw", k_pair_split<E, 4, 16384, 2, true, 6623>, 128, 4, 128 - 2 * E},
+      {"test_sep", k_pair_split<E, 4, 0, 2, true, 6623 | 32768>, 128, 4, 128 - 2 * E},
+      {"prod", k_pair_split<E, 4, 0, 2, false, 6623>, 128, 4, 128 - 2 * E},
+  };
 #elif defined(PB_SET_BIG)
   // -DPB_SET_BIG: the multi-round regime (16384^2 / 32768^2 as one block, the
   // host launches without the wave priority): round-4 NP (7) against the
@@ -343,6 +354,81 @@ int main(int argc, char **argv) {
         cur = 1 - cur;
       }
     };
+#if defined(PB_SET_TESTABL)
+    // test mode: an L_h[W0] field in the block layout and the sin tables
+    static double *lwb = nullptr, *dsx = nullptr, *dsy = nullptr;
+    if (!lwb) {
+      CK(hipMalloc(&lwb, bytes));
+      CK(hipMemset(lwb, 0, bytes));
+      std::vector<double> t(n + 4 * E);
+      for (int g = 0; g < n + 4 * E; ++g) t[g] = std::sin(2 * M_PI * ((g - E) * dh));
+      CK(hipMalloc(&dsx, t.size() * 8));
+      CK(hipMalloc(&dsy, t.size() * 8));
+      CK(hipMemcpy(dsx, t.data(), t.size() * 8, hipMemcpyHostToDevice));
+      CK(hipMemcpy(dsy, t.data(), t.size() * 8, hipMemcpyHostToDevice));
+    }
+    // the separable L_h[W0] tables (nlh_device.h StepConst lsx / lty) and,
+    // for the DMA variants, the same L_h[W0] field (long double, rounded)
+    static double *dlsx = nullptr, *dlty = nullptr;
+    if (!dlsx) {
+      constexpr int NLV = pair_sep_nlv(E), LTS = pair_sep_stride(E);
+      const int64_t ncol = pair_sep_ncol(E, n);
+      auto sxe = [&](int64_t g) -> long double { return (g >= 0 && g < n) ? (long double)std::sin(2 * M_PI * (g * dh)) : 0.0L; };
+      std::vector<double> lsx((NLV + 1) * ncol, 0.0), lty((size_t)(n + 4 * E) * LTS, 0.0);
+      std::vector<long double> sxp((NLV + 1) * ncol, 0.0L), tyl((size_t)(n + 4 * E) * LTS, 0.0L);
+      for (int64_t c = 0; c < ncol; ++c) {
+        const int64_t g = c - 2 * E;
+        if (g < 0 || g >= n) continue;
+        for (int l = 0; l < NLV; ++l) {
+          const int Lv = pair_sep_level(E, l);
+          long double sum = 0.0L;
+          for (int dx = -Lv; dx <= Lv; ++dx) sum += sxe(g + dx);
+          sxp[l * ncol + c] = sum - (2 * Lv + 1) * sxe(g);
+        }
+        sxp[NLV * ncol + c] = sxe(g);
+      }
+      for (int64_t r = 0; r < n + 4 * E; ++r) {
+        const int64_t y = r - 2 * E;
+        if (y < 0 || y >= n) continue;
+        for (int l = 0; l < NLV; ++l) {
+          long double sum = 0.0L;
+          for (int d = -E; d <= E; ++d)
+            if (clen(E, d < 0 ? -d : d) == pair_sep_level(E, l)) sum += sxe(y + d);
+          tyl[r * LTS + l] = sum;
+        }
+        long double z = -(long double)disk * sxe(y);
+        for (int d = -E; d <= E; ++d) z += (2 * clen(E, d < 0 ? -d : d) + 1) * sxe(y + d);
+        tyl[r * LTS + NLV] = z;
+      }
+      const long double cdl = (long double)C.c2d * (long double)C.dh2;  // folded into Sx' and sx
+      for (size_t i = 0; i < lsx.size(); ++i) lsx[i] = (double)(sxp[i] * cdl);
+      for (size_t i = 0; i < lty.size(); ++i) lty[i] = (double)tyl[i];
+      CK(hipMalloc(&dlsx, lsx.size() * 8));
+      CK(hipMalloc(&dlty, lty.size() * 8));
+      CK(hipMemcpy(dlsx, lsx.data(), lsx.size() * 8, hipMemcpyHostToDevice));
+      CK(hipMemcpy(dlty, lty.data(), lty.size() * 8, hipMemcpyHostToDevice));
+      // the L_h[W0] field over the stage-1 rows / columns of every block row
+      const long double cd = (long double)C.c2d * (long double)C.dh2;
+      std::vector<double> lwh((size_t)pitch * rows, 0.0);
+      for (int64_t y = -E; y < n + E; ++y)
+        for (int64_t x = -E; x < n + E; ++x) {
+          if (y < 0 || y >= n || x < 0 || x >= n) continue;
+          long double v = sxp[NLV * ncol + x + 2 * E] * tyl[(y + 2 * E) * LTS + NLV];
+          for (int l = 0; l < NLV; ++l) v += sxp[l * ncol + x + 2 * E] * tyl[(y + 2 * E) * LTS + l];
+          lwh[(size_t)((y + H + kPairPadRows) * pitch + XL + x)] = (double)(cd * v);
+        }
+      CK(hipMemcpy(lwb, lwh.data(), lwh.size() * 8, hipMemcpyHostToDevice));
+    }
+    C.lsx = dlsx;
+    C.lty = dlty;
+    L.r[0].lw = origin(lwb);
+    C.sxt = dsx;
+    C.syt = dsy;
+    C.st2pi = 0.1;
+    C.ct = 0.9;
+    C.st2pi2 = 0.11;
+    C.ct2 = 0.89;
+#endif
 #if defined(PB_SET_TRACE)
     // every launch of an ABL 2048 variant writes its per-wave records through
     // Rc.lw: the buffer exists before the first launch (round 5: a launch with
