@@ -79,16 +79,19 @@ constexpr int kPairSplitB = 4;  // k_pair_split: rows per barrier
 // rings whose slot counts divide the period (production; E = 8: 27.7 KB of
 // LDS per workgroup, 4 per CU): 67.62 -> 66.44 us (profiles/r05/pair/ring_*).
 // 512 (harness only) puts wave 0 at the wave priority instead of wave 1;
-// 1024 (harness only) the lean stage 2 (spills).  32768 (test mode, E = 8):
-// the L_h[W0] rows from the separable form L_h[W0] = sum_l Sx'_l(x) Ty_l(y)
-// + sx(x) Z(y) (StepConst lsx / lty) -- per row a 64-byte Ty / Z DMA instead
-// of the 1-KB L_h[W0] row, wave 1 forming the row B iterations ahead of wave
-// 0: C2 test-mode harness 98.9 -> 94.7 us per pass, 4.4e-16 from the field
-// (profiles/r05/pair/test_sep2_reps4.jsonl; the row DMA itself costs 15%).
+// 1024 (harness only) the lean stage 2 (spills).  32768 (test mode, E = 8;
+// off): the L_h[W0] rows from the separable form L_h[W0] = sum_l Sx'_l(x)
+// Ty_l(y) + sx(x) Z(y) (StepConst lsx / lty) -- per row a 64-byte Ty / Z DMA
+// instead of the 1-KB L_h[W0] row, wave 1 forming the row B iterations ahead
+// of wave 0: C2 test-mode harness 98.9 -> 94.7 us per pass, 4.4e-16 from the
+// field (profiles/r05/pair/test_sep2_reps4.jsonl), but in the library build
+// 96.5 -> 103.9 us per pass (rocprofv3, 51.1 vs 46.0 VALU lane-ops per
+// node-update; profiles/r05/evidence_2c33717e/test), so the library keeps
+// the L_h[W0] row DMA.
 constexpr int kPairPadRows = 16;
 __host__ __device__ constexpr bool pair_rows(int E);
 __host__ __device__ constexpr int pair_opt(int E) {
-  return E == 8 ? 15 | 16 | 64 | 128 | 256 | 2048 | 4096 | 32768
+  return E == 8 ? 15 | 16 | 64 | 128 | 256 | 2048 | 4096
                 : (E == 13 ? 14 | 16 : (E <= 12 && pair_rows(E) ? 15 | 16 | 64 : 15 | 16));
 }
 
