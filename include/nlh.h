@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define NLH_ABI_VERSION 9
+#define NLH_ABI_VERSION 10
 
 enum nlh_status {
   NLH_OK = 0,
@@ -151,6 +151,27 @@ int nlh_snapshot_wait(nlh_solver *s, double *u_global);
  * Asynchronous: returns once the work is enqueued (nlh_synchronize waits). */
 int nlh_run(nlh_solver *s, int64_t nsteps);
 int nlh_synchronize(nlh_solver *s);
+/* Host-side timing of the last nlh_run and the nlh_synchronize after it, in
+ * microseconds from nlh_run's entry (the reference times do_work with the
+ * host clock, src/2d_nonlocal_serial.cpp:362-367; this splits that interval):
+ *   enqueue_us      nlh_run returned (its launches are enqueued)
+ *   start_seen_us   the run's start event seen complete (NLH_HOST_PROBE=1
+ *                   diagnostics only; -1 otherwise)
+ *   end_seen_us     nlh_synchronize first saw the run's end event complete
+ *                   (kernel timing 1, polling waits; -1 otherwise)
+ *   sync_return_us  nlh_synchronize returned (-1 if not called since)
+ *   event_span_us   the run's HIP event pair on the stencil stream (kernel
+ *                   timing 1 / 3; -1 otherwise)
+ * sync_mode: NLH_SYNC (0 = nlh_synchronize polls the streams itself and
+ * leaves the device's host-wait flag alone; 1-4 = the flag set to yield /
+ * blocking / auto / spin and hipStreamSynchronize).                        */
+typedef struct nlh_host_times {
+  double enqueue_us, start_seen_us, end_seen_us, sync_return_us, event_span_us;
+  int32_t sync_mode;
+  int32_t reserved_;
+} nlh_host_times;
+int nlh_host_time(nlh_solver *s, nlh_host_times *out);
+
 /* Current step index t (the field holds u(t)).                            */
 int64_t nlh_step_index(const nlh_solver *s);
 

@@ -85,6 +85,14 @@ class _PhaseTimes(ctypes.Structure):
     ]
 
 
+class _HostTimes(ctypes.Structure):
+    _fields_ = [
+        ("enqueue_us", ctypes.c_double), ("start_seen_us", ctypes.c_double), ("end_seen_us", ctypes.c_double),
+        ("sync_return_us", ctypes.c_double), ("event_span_us", ctypes.c_double), ("sync_mode", ctypes.c_int32),
+        ("reserved_", ctypes.c_int32),
+    ]
+
+
 class _Params1D(ctypes.Structure):
     _fields_ = [
         ("nx", ctypes.c_int64), ("eps", ctypes.c_int64),
@@ -110,6 +118,7 @@ _SIGNATURES = {
     "nlh_snapshot_wait": ([ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
     "nlh_synchronize": ([ctypes.c_void_p], ctypes.c_int),
     "nlh_step_index": ([ctypes.c_void_p], ctypes.c_int64),
+    "nlh_host_time": ([ctypes.c_void_p, ctypes.POINTER(_HostTimes)], ctypes.c_int),
     "nlh_errors": ([ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_double),
                     ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
     "nlh_get_info": ([ctypes.c_void_p, ctypes.POINTER(_Info)], ctypes.c_int),
@@ -533,6 +542,17 @@ class Solver:
         if rc < 0:
             _check(-rc, "nlh_rebalance")
         return rc, out, bo
+
+    def host_time(self) -> dict:
+        """Host-side split of the last run() + synchronize() (nlh_host_time),
+        microseconds from run()'s entry: enqueue (run returned), start_seen
+        (NLH_HOST_PROBE=1 only), end_seen (the run's end event first seen by
+        the polling wait, kernel timing 1), sync_return, and the run's event
+        span on the stencil stream; -1 where not recorded."""
+        t = _HostTimes()
+        _check(lib().nlh_host_time(self._h, ctypes.byref(t)), "nlh_host_time")
+        return {"enqueue_us": t.enqueue_us, "start_seen_us": t.start_seen_us, "end_seen_us": t.end_seen_us,
+                "sync_return_us": t.sync_return_us, "event_span_us": t.event_span_us, "sync_mode": t.sync_mode}
 
     def kernel_time(self):
         """(summed stencil-pass milliseconds, time steps those passes advanced)."""

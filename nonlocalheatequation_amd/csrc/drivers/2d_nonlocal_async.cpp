@@ -39,7 +39,9 @@ static int solve(int64_t nx, int64_t ny, int64_t np, int64_t nt, int64_t eps, do
   p.nranks = 1;
   p.tiles_x = np;
   p.tiles_y = np;
+  p.kernel = driver_kernel(p, nt);
   if (nlh_create(&p, out) != NLH_OK) return die("nlh_create");
+  note_fast_test_kernel(*out, p, kernel, true);
   // the partition_space constructor always applies the sin*sin IC (:70-78)
   if (nlh_init_test(*out) != NLH_OK) return die("nlh_init_test");
   Logger lg;

@@ -70,7 +70,9 @@ static int make_solver(const Run &r, const RankEnv &re, const uint8_t *id, int k
     if (v >= owners_of(re)) v %= owners_of(re);  // a map written for more localities than ranks
   p.owner = own.empty() ? nullptr : own.data();
   p.comm_id = re.nranks > 1 ? id : nullptr;
+  p.kernel = driver_kernel(p, r.nt);
   if (nlh_create(&p, out) != NLH_OK) return die("nlh_create");
+  note_fast_test_kernel(*out, p, kernel, re.rank == 0);
   if (nlh_init_test(*out) != NLH_OK) return die("nlh_init_test");
   return 0;
 }
@@ -196,8 +198,11 @@ int main(int argc, char **argv) {
   // balance point and keeps the overlapped exchange schedule elsewhere
   // (ADVICE r4); --test_load_balance reports rates over the whole run, so
   // there it stays on throughout
+  // (at most the interval itself: --nbalance 1 measures every step)
   const int64_t busy_window =
-      (balancing && !lb_test) ? std::max<int64_t>(2, std::min<int64_t>(64, (nbalance / 4 + 1) & ~int64_t(1))) : 0;
+      (balancing && !lb_test)
+          ? std::min<int64_t>(nbalance, std::max<int64_t>(2, std::min<int64_t>(64, (nbalance / 4 + 1) & ~int64_t(1))))
+          : 0;
   if ((lb_test || (balancing && busy_window == 0)) && nlh_kernel_timing(s, 2) != NLH_OK)
     return die("nlh_kernel_timing");
   auto on_window = [&](int64_t) -> int { return nlh_kernel_timing(s, 2); };

@@ -48,8 +48,10 @@ static int batch_tester(int64_t nlog, int kernel, int device) {
     double k, dt, dh;
     std::cin >> nx >> ny >> nt >> eps >> k >> dt >> dh;
     nlh_params p = make_params(nx, ny, eps, k, dt, dh, true, kernel, device);
+    p.kernel = driver_kernel(p, (int64_t)nt);
     nlh_solver *s = nullptr;
     if (nlh_create(&p, &s) != NLH_OK) return die("nlh_create");
+    note_fast_test_kernel(s, p, kernel, true);
     if (nlh_init_test(s) != NLH_OK) return die("nlh_init_test");
     Logger lg;
     lg.nx = nx, lg.ny = ny, lg.dt = dt, lg.dh = dh, lg.test = true;
@@ -108,8 +110,10 @@ int main(int argc, char **argv) {
 
   const bool test = o.count("test");
   nlh_params p = make_params(nx, ny, eps, k, dt, dh, test, kernel, device);
+  p.kernel = driver_kernel(p, (int64_t)nt);
   nlh_solver *s = nullptr;
   if (nlh_create(&p, &s) != NLH_OK) return die("nlh_create");
+  note_fast_test_kernel(s, p, kernel, true);
   if (test) {
     if (nlh_init_test(s) != NLH_OK) return die("nlh_init_test");
   } else {  // input_init: nx*ny values, sx outer (:180-187)

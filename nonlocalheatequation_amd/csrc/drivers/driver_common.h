@@ -65,6 +65,20 @@ RankEnv rank_env();
 bool share_comm_id(const RankEnv &re, uint8_t id[NLH_COMM_ID_BYTES], std::string &err, bool fresh = true);
 
 int kernel_from_name(const std::string &s);
+
+// --kernel auto in test mode: the drivers print the
+// reference's l2 / linfinity, which the FAST kernels reproduce only to the
+// L2 contract of include/nlh.h.  Where the EXACT kernel's whole run is cheap
+// -- nx*ny*nt*N(eps) <= kDriverExactTerms disk terms, well under a second on
+// one MI355X -- AUTO becomes EXACT, so the printed numbers are the
+// reference's own order bit for bit (every row of the reference's batch
+// files).  Returns the kernel to request.
+constexpr double kDriverExactTerms = 2e11;
+int driver_kernel(const nlh_params &p, int64_t nt);
+// after nlh_create: when the run prints test-mode errors from a FAST kernel
+// that --kernel auto chose, one line on stderr names the kernel and the
+// contract its l2 follows
+void note_fast_test_kernel(nlh_solver *s, const nlh_params &p, int requested, bool print);
 // --influence constant|linear -> enum nlh_influence (-1 if unknown)
 int influence_from_name(const std::string &s);
 

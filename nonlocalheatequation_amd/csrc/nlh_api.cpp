@@ -170,7 +170,10 @@ constexpr EnvKnob kEnvKnobs[] = {
     {"NLH_PITCH_PAD", 0, 1024},    // extra doubles per padded row
     {"NLH_BAND_SEG", 0, 1 << 20},  // edge-band segment height (0 = automatic)
     {"NLH_COMM_INIT_TIMEOUT", 1, 86400},  // seconds a communicator init may take (default 300)
-    {"NLH_SYNC", 0, 3},            // host waits: 0 spin (default), 1 yield, 2 blocking, 3 HIP's auto
+    {"NLH_SYNC", 0, 4},            // nlh_synchronize: 0 polls the streams (default), 1-4 set the device's
+                                   // host-wait flag (yield, blocking, auto, spin) and block in HIP
+    {"NLH_HOST_PROBE", 0, 1},      // diagnostics: nlh_run spins until its first launch has started
+    {"NLH_GRAPH", 0, 1},           // 1: production passes replayed from captured HIP graphs
     {"NLH_PAIR_PRIO", 0, 2},       // k_pair_split wave priority: 0 never, 1 one-round lists (default), 2 not on bands
     {"NLH_TRACE_REPART", 0, 1},    // repartition phase times on stderr
 };
@@ -277,7 +280,8 @@ struct nlh_solver {
   bool weighted = false;  // k_weighted: non-constant influence function
   bool prefix = false;    // k_prefix_rt (nlh_prefix.h) past the k_wide horizons
   int32_t *d_ptab = nullptr;  // k_prefix_rt's per-offset prefix index table
-  double *d_lsx = nullptr, *d_lty = nullptr;  // two-step test mode: separable L_h[W0] tables (sep_tables)
+  double *d_lsx = nullptr, *d_lty = nullptr;  // fast test mode, J = 1: separable L_h[W0] tables (sep_tables)
+  int sep_nlv = 0, sep_lts = 0;                // their level count and lty row stride
   double *d_wt = nullptr, *d_qj = nullptr;  // J tables (influence != 0)
   int halo = 0;       // halo rows/columns held per block: eps, or 2*eps with pair
   // production k_pair_split rings: 6 = D4/B2 (default; with row pairs 444-450 vs 438-446 G
@@ -356,9 +360,33 @@ struct nlh_solver {
   hipEvent_t ev_snap_dev = nullptr, ev_snap = nullptr;
   double *snap_dev = nullptr, *snap_host = nullptr;
   Flag snap_pending;
+  // host waits and host-side timing (nlh_host_time): steady-clock ns of the
+  // last nlh_run's entry / return, of nlh_synchronize's first observation of
+  // that run's end event (timing 1) and of its return
+  int sync_mode = 0;        // NLH_SYNC (kEnvKnobs)
+  bool host_probe = false;  // NLH_HOST_PROBE: record when the run's start event completes
+  int64_t h_enter = 0, h_return = 0, h_start_seen = -1, h_end_seen = -1, h_sync_return = 0;
+  hipEvent_t h_e0 = nullptr, h_e1 = nullptr;  // the last nlh_run's event pair (timing 1 / 3)
+  // HIP graphs of production passes (NLH_GRAPH=1): runs of g passes (g a
+  // power of two, 2 .. kGraphMaxPasses) starting at buffer parity k, captured
+  // on first use and replayed by one hipGraphLaunch each (capture_graph)
+  struct Graph {
+    int passes = 0, k = 0;
+    hipGraphExec_t exec = nullptr;
+  };
+  bool graph_on = false;
+  std::vector<Graph> graphs;
+  int64_t passes_enqueued = 0;  // ungraphed passes since creation (RCCL peers connected before capture)
+  bool capture_first = false;   // capturing the graph's first pass: no waits on events recorded outside it
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_join2 = nullptr;
 };
 
 namespace {
+
+int64_t now_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
 
 int set_device(const nlh_solver *s) {
   HIP_TRY(hipSetDevice(s->device));
@@ -860,6 +888,10 @@ int enqueue_step(nlh_solver *s, int nsteps) {
       if ((rc = enqueue_exchange(s, k))) return rc;
       s->halo_fresh = true;
     }
+    // a graph's first pass: the launch itself is ordered after every
+    // earlier pass on all streams (launch_graph), and events recorded outside
+    // the capture cannot be waited on inside it
+    const bool outside = !s->capture_first;
     if (s->timing == 2) {
       // busy timing: the pass serialised on s_main -- halo(n), every rank's
       // bands, every rank's interior -- so each rank's pairs time its own
@@ -874,7 +906,7 @@ int enqueue_step(nlh_solver *s, int nsteps) {
     } else if (s->sched == 1) {
       // bands(n) then interior(n), both on s_main: the bands run alone
       // briefly and the interior keeps its one-round grid
-      HIP_TRY(hipStreamWaitEvent(s->s_main, s->ev_halo, 0));  // halo(n)
+      if (outside) HIP_TRY(hipStreamWaitEvent(s->s_main, s->ev_halo, 0));  // halo(n)
       if ((rc = stencil(s->rl_bnd[k], s->pl_bnd[k], s->s_main, kEvBand))) return rc;
       HIP_TRY(hipEventRecord(s->ev_band, s->s_main));
       if ((rc = stencil(s->rl_int[k], s->pl_int[k], s->s_main, kEvInterior))) return rc;
@@ -884,8 +916,10 @@ int enqueue_step(nlh_solver *s, int nsteps) {
       // the chain bands -> pack -> send/recv -> unpack -> next bands crosses
       // no queue; only interior(n-1) -> bands(n) and bands(n-1) -> interior(n)
       // do (about 11 us per cross-queue wait, profiles/r01/sched)
-      HIP_TRY(hipStreamWaitEvent(s->s_main, s->ev_band, 0));  // bands(n-1)
-      HIP_TRY(hipStreamWaitEvent(s->s_comm, s->ev_int, 0));   // interior(n-1)
+      if (outside) {
+        HIP_TRY(hipStreamWaitEvent(s->s_main, s->ev_band, 0));  // bands(n-1)
+        HIP_TRY(hipStreamWaitEvent(s->s_comm, s->ev_int, 0));   // interior(n-1)
+      }
       if ((rc = stencil(s->rl_int[k], s->pl_int[k], s->s_main, kEvInterior))) return rc;
       HIP_TRY(hipEventRecord(s->ev_int, s->s_main));
       if ((rc = stencil(s->rl_bnd[k], s->pl_bnd[k], s->s_comm, kEvBand))) return rc;
@@ -895,9 +929,11 @@ int enqueue_step(nlh_solver *s, int nsteps) {
       s->t += nsteps;
       return NLH_OK;
     } else {
-      HIP_TRY(hipStreamWaitEvent(s->s_main, s->ev_band, 0));  // bands(n-1)
-      HIP_TRY(hipStreamWaitEvent(s->s_band, s->ev_int, 0));   // interior(n-1)
-      HIP_TRY(hipStreamWaitEvent(s->s_band, s->ev_halo, 0));  // halo(n)
+      if (outside) {
+        HIP_TRY(hipStreamWaitEvent(s->s_main, s->ev_band, 0));  // bands(n-1)
+        HIP_TRY(hipStreamWaitEvent(s->s_band, s->ev_int, 0));   // interior(n-1)
+        HIP_TRY(hipStreamWaitEvent(s->s_band, s->ev_halo, 0));  // halo(n)
+      }
       if ((rc = stencil(s->rl_int[k], s->pl_int[k], s->s_main, kEvInterior))) return rc;
       HIP_TRY(hipEventRecord(s->ev_int, s->s_main));
       if ((rc = stencil(s->rl_bnd[k], s->pl_bnd[k], s->s_band, kEvBand))) return rc;
@@ -912,11 +948,24 @@ int enqueue_step(nlh_solver *s, int nsteps) {
 }
 
 int compute_lw(nlh_solver *s) {
-  // L_h[W0](x) = sum_disk c*(W0~_j - W0_x)*dh^2 with the exact per-term
-  // order; the fast test-mode source is then b = -(2pi st) W0 - ct L_h[W0].
-  // With the two-step kernel (halo 2E) also over the block's E-wide frame:
-  // stage 1 computes u^{t+1} there
+  // L_h[W0](x) = sum_disk c*(W0~_j - W0_x)*dh^2; the fast test-mode source is
+  // then b = -(2pi st) W0 - ct L_h[W0].  With the two-step kernel (halo 2E)
+  // also over the block's E-wide frame: stage 1 computes u^{t+1} there.
+  // J = 1 (round 6): from the separable long-double tables (k_lw_sep), the
+  // disk sum without the rounding of its N(eps) sequential terms -- at eps
+  // 200 that rounding alone put the fast test mode 1.09e-12 of field scale
+  // from the compensated oracle at the stable dt (tests/test_gpu_stable_dt.py)
+  // -- and O(levels) per node instead of O(N(eps)).  J != 1: the exact
+  // per-term order (k_exact's sum)
   const int ext = s->pair ? (int)s->p.eps : 0;
+  if (s->d_lty) {
+    for (auto &b : s->blocks)
+      if (nlh::launch_lw_sep(b.lw_origin(), b.pitch, -ext, -ext, (int)b.r.w + 2 * ext, (int)b.r.h + 2 * ext,
+                             (int)b.r.x0, (int)b.r.y0, s->sc, s->sep_nlv, s->sep_lts, s->s_main))
+        return fail(NLH_ERR_HIP, "L_h[W0] launch");
+    HIP_TRY(hipStreamSynchronize(s->s_main));
+    return NLH_OK;
+  }
   for (auto &b : s->blocks) {
     double *tmp = b.base[1];
     // the whole buffer: rows above the block as origin() counts them
@@ -980,6 +1029,11 @@ void release_impl(nlh_solver *s, bool keep_comm) {
   if (s->s_band) (void)hipStreamSynchronize(s->s_band);
   if (s->s_copy) (void)hipStreamSynchronize(s->s_copy);
   trace_mark("r_sync");
+  for (auto &g : s->graphs) (void)hipGraphExecDestroy(g.exec);
+  s->graphs.clear();
+  if (s->ev_fork) (void)hipEventDestroy(s->ev_fork);
+  if (s->ev_join) (void)hipEventDestroy(s->ev_join);
+  if (s->ev_join2) (void)hipEventDestroy(s->ev_join2);
   if (s->comm && !keep_comm) ncclCommDestroy(s->comm);
   (void)hipFree(s->snap_dev);
   if (s->snap_host) (void)hipHostFree(s->snap_host);
@@ -1053,46 +1107,59 @@ void swap_queues(nlh_solver *a, nlh_solver *b) {
 int sep_tables(nlh_solver *s, const std::vector<int32_t> &lens) {
   const nlh_params &p = s->p;
   const int E = (int)p.eps;
-  std::vector<int> lev;  // = nlh_pair.h pair_sep_level(E, l)
+  std::vector<int> lev;                // = nlh_pair.h pair_sep_level(E, l)
+  std::vector<int> lev_of(E + 1, -1);  // half-width -> level index
   for (int d = 0, prev = -1; d <= E; ++d) {
-    if (lens[d] > 0 && lens[d] != prev) lev.push_back(lens[d]);
+    if (lens[d] > 0 && lens[d] != prev) {
+      lev_of[lens[d]] = (int)lev.size();
+      lev.push_back(lens[d]);
+    }
     prev = lens[d];
   }
   const int nlv = (int)lev.size(), lts = nlh::pair_sep_stride_n(nlv);
   const int64_t ncol = nlh::pair_sep_ncol(E, p.nx);
-  auto sx = [&](int64_t g) -> long double { return (g >= 0 && g < p.nx) ? (long double)sin(2 * M_PI * (g * p.dh)) : 0.0L; };
-  auto sy = [&](int64_t g) -> long double { return (g >= 0 && g < p.ny) ? (long double)sin(2 * M_PI * (g * p.dh)) : 0.0L; };
+  // the glibc sin values the kernels use (zero-extended), their long-double
+  // prefix sums along x: Sx_L(g) = P(g + L + 1) - P(g - L) in O(1) (round 5
+  // summed 2L + 1 sin calls per column and level: O(nx E^2))
+  std::vector<long double> sxl(p.nx), syl(p.ny), px(p.nx + 1, 0.0L);
+  for (int64_t g = 0; g < p.nx; ++g) sxl[g] = (long double)sin(2 * M_PI * (g * p.dh));
+  for (int64_t g = 0; g < p.ny; ++g) syl[g] = (long double)sin(2 * M_PI * (g * p.dh));
+  for (int64_t g = 0; g < p.nx; ++g) px[g + 1] = px[g] + sxl[g];
+  auto win = [&](int64_t g, int L) {
+    return px[std::min<int64_t>(g + L + 1, p.nx)] - px[std::max<int64_t>(g - L, 0)];
+  };
   const long double cd = (long double)s->sc.c2d * (long double)s->sc.dh2;
   std::vector<double> lsx((size_t)(nlv + 1) * ncol, 0.0), lty((size_t)(p.ny + 4 * E) * lts, 0.0);
-  for (int64_t c = 0; c < ncol; ++c) {
-    const int64_t g = c - 2 * E;
-    if (g < 0 || g >= p.nx) continue;
-    for (int l = 0; l < nlv; ++l) {
-      long double sum = 0.0L;
-      for (int dx = -lev[l]; dx <= lev[l]; ++dx) sum += sx(g + dx);
-      lsx[(size_t)l * ncol + c] = (double)(cd * (sum - (2 * lev[l] + 1) * sx(g)));
-    }
-    lsx[(size_t)nlv * ncol + c] = (double)(cd * sx(g));
+  for (int64_t g = 0; g < p.nx; ++g) {
+    const int64_t c = g + 2 * E;
+    for (int l = 0; l < nlv; ++l)
+      lsx[(size_t)l * ncol + c] = (double)(cd * (win(g, lev[l]) - (2 * lev[l] + 1) * sxl[g]));
+    lsx[(size_t)nlv * ncol + c] = (double)(cd * sxl[g]);
   }
-  for (int64_t r = 0; r < p.ny + 4 * E; ++r) {
-    const int64_t y = r - 2 * E;
-    if (y < 0 || y >= p.ny) continue;
-    long double z = -(long double)s->disk * sy(y);
-    for (int d = -E; d <= E; ++d) z += (2 * lens[d < 0 ? -d : d] + 1) * sy(y + d);
-    for (int l = 0; l < nlv; ++l) {
-      long double sum = 0.0L;
-      for (int d = -E; d <= E; ++d)
-        if (lens[d < 0 ? -d : d] == lev[l]) sum += sy(y + d);
-      lty[(size_t)r * lts + l] = (double)sum;
+  std::vector<long double> ty(nlv);
+  for (int64_t y = 0; y < p.ny; ++y) {
+    long double z = -(long double)s->disk * syl[y];
+    std::fill(ty.begin(), ty.end(), 0.0L);
+    for (int d = -E; d <= E; ++d) {
+      const int64_t yy = y + d;
+      if (yy < 0 || yy >= p.ny) continue;
+      const int L = lens[d < 0 ? -d : d];
+      z += (2 * L + 1) * syl[yy];
+      if (L > 0) ty[lev_of[L]] += syl[yy];
     }
-    lty[(size_t)r * lts + nlv] = (double)z;
+    const size_t r = (size_t)(y + 2 * E) * lts;
+    for (int l = 0; l < nlv; ++l) lty[r + l] = (double)ty[l];
+    lty[r + nlv] = (double)z;
   }
   HIP_TRY(hipMalloc(&s->d_lsx, lsx.size() * sizeof(double)));
   HIP_TRY(hipMalloc(&s->d_lty, lty.size() * sizeof(double)));
   HIP_TRY(hipMemcpy(s->d_lsx, lsx.data(), lsx.size() * sizeof(double), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(s->d_lty, lty.data(), lty.size() * sizeof(double), hipMemcpyHostToDevice));
+  s->device_bytes += (int64_t)((lsx.size() + lty.size()) * sizeof(double));
   s->sc.lsx = s->d_lsx;
   s->sc.lty = s->d_lty;
+  s->sep_nlv = nlv;
+  s->sep_lts = lts;
   return NLH_OK;
 }
 
@@ -1134,19 +1201,22 @@ int create_impl(const nlh_params *pin, nlh_solver *s, ncclComm_t reuse_comm = nu
     HIP_TRY(hipGetDevice(&s->device));
   }
   HIP_TRY(hipSetDevice(s->device));
-  // host waits (nlh_synchronize, event waits) spin by default: a blocking or
-  // yielding wait wakes tens of microseconds after the GPU finishes, ~4% of
-  // a 20-step C2 run (r05).  Only a device whose context is not yet active
-  // takes the flag; otherwise HIP keeps what it has (error cleared)
-  {
-    int mode = 0;
-    if (const char *v = std::getenv("NLH_SYNC"))
-      if (*v) mode = std::atoi(v);
-    const unsigned fl = mode == 1 ? hipDeviceScheduleYield
-                        : mode == 2 ? hipDeviceScheduleBlockingSync
-                        : mode == 3 ? hipDeviceScheduleAuto : hipDeviceScheduleSpin;
+  // host waits: nlh_synchronize polls its streams itself (NLH_SYNC unset or
+  // 0), so the process-wide host-wait flag of the device stays the
+  // application's.  NLH_SYNC=1..4 (A/B diagnostics) sets the flag
+  // -- taken only by a device whose context is not yet active; otherwise HIP
+  // keeps what it has (error cleared) -- and blocks in hipStreamSynchronize
+  s->sync_mode = 0;
+  if (const char *v = std::getenv("NLH_SYNC"))
+    if (*v) s->sync_mode = std::atoi(v);
+  if (s->sync_mode != 0) {
+    const unsigned fl = s->sync_mode == 1 ? hipDeviceScheduleYield
+                        : s->sync_mode == 2 ? hipDeviceScheduleBlockingSync
+                        : s->sync_mode == 3 ? hipDeviceScheduleAuto : hipDeviceScheduleSpin;
     if (hipSetDeviceFlags(fl) != hipSuccess) (void)hipGetLastError();
   }
+  if (const char *v = std::getenv("NLH_HOST_PROBE")) s->host_probe = *v && std::atoi(v) != 0;
+  if (const char *v = std::getenv("NLH_GRAPH")) s->graph_on = *v && std::atoi(v) != 0;
   hipDeviceProp_t prop;
   HIP_TRY(hipGetDeviceProperties(&prop, s->device));
   std::snprintf(s->arch, sizeof(s->arch), "%s", prop.gcnArchName);
@@ -1265,7 +1335,7 @@ int create_impl(const nlh_params *pin, nlh_solver *s, ncclComm_t reuse_comm = nu
     HIP_TRY(hipMalloc(&s->d_ptab, tab.size() * sizeof(int32_t)));
     HIP_TRY(hipMemcpy(s->d_ptab, tab.data(), tab.size() * sizeof(int32_t), hipMemcpyHostToDevice));
   }
-  if (s->pair && p.test) {
+  if (kern == NLH_KERNEL_FAST && p.test && p.influence == NLH_INFLUENCE_CONSTANT) {  // compute_lw's L_h[W0]
     int rc2 = sep_tables(s, lens);
     if (rc2) return rc2;
   }
@@ -1746,6 +1816,143 @@ int fold_events(nlh_solver *s, bool drain) {
   return NLH_OK;
 }
 
+// ---- HIP graphs of production passes (NLH_GRAPH=1)
+// A run of g passes is captured once per (g, start parity) and replayed with
+// one hipGraphLaunch on s_main: the pass launches, and with an exchange every
+// pass's interior / bands / pack / grouped ncclSend-ncclRecv / unpack on the
+// streams and with the cross-stream events of the ungraphed schedule (the
+// side streams fork from s_main at the start and join it at the end), so the
+// host enqueues one launch per g passes instead of each pass's kernels,
+// events and RCCL calls.  The kernels and their arguments are the ungraphed
+// ones: bitwise equal fields.  Production mode only (test mode's per-step
+// source constants are kernel arguments), kernel timing 0 / 1 only, and only
+// once the halo is fresh and an ungraphed exchange has connected RCCL's peers.
+constexpr int kGraphMaxPasses = 16;
+
+int graph_passes(const nlh_solver *s, int64_t passes_left) {
+  if (!s->graph_on || s->p.test || (s->timing != 0 && s->timing != 1)) return 0;
+  if (s->exchange && (!s->halo_fresh || s->passes_enqueued < 2)) return 0;
+  int g = 0;
+  for (int c = 2; c <= kGraphMaxPasses && c <= passes_left; c *= 2) g = c;
+  return g;
+}
+
+int capture_graph(nlh_solver *s, int g, int spp, hipGraphExec_t *out) {
+  if (s->exchange && !s->ev_fork) {
+    HIP_TRY(hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&s->ev_join, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&s->ev_join2, hipEventDisableTiming));
+  }
+  const int64_t t0 = s->t, steps0 = s->timed_steps, passes0 = s->timed_passes;
+  const int cur0 = s->cur;
+  const bool band_stream = s->exchange && s->sched == 0;
+  HIP_TRY(hipStreamBeginCapture(s->s_main, hipStreamCaptureModeRelaxed));
+  int rc = NLH_OK;
+  auto body = [&]() -> int {
+    if (s->exchange) {
+      HIP_TRY(hipEventRecord(s->ev_fork, s->s_main));
+      HIP_TRY(hipStreamWaitEvent(s->s_comm, s->ev_fork, 0));
+      if (band_stream) HIP_TRY(hipStreamWaitEvent(s->s_band, s->ev_fork, 0));
+    }
+    for (int j = 0; j < g; ++j) {
+      s->capture_first = j == 0;
+      const int r = enqueue_step(s, spp);
+      s->capture_first = false;
+      if (r) return r;
+    }
+    if (s->exchange) {
+      HIP_TRY(hipEventRecord(s->ev_join, s->s_comm));
+      HIP_TRY(hipStreamWaitEvent(s->s_main, s->ev_join, 0));
+      if (band_stream) {
+        HIP_TRY(hipEventRecord(s->ev_join2, s->s_band));
+        HIP_TRY(hipStreamWaitEvent(s->s_main, s->ev_join2, 0));
+      }
+    }
+    return NLH_OK;
+  };
+  rc = body();
+  hipGraph_t graph = nullptr;
+  const hipError_t ec = hipStreamEndCapture(s->s_main, &graph);
+  s->t = t0;
+  s->cur = cur0;
+  s->timed_steps = steps0;
+  s->timed_passes = passes0;
+  if (rc) {
+    if (graph) (void)hipGraphDestroy(graph);
+    return rc;
+  }
+  if (ec != hipSuccess) return fail(NLH_ERR_HIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(ec));
+  const hipError_t ei = hipGraphInstantiate(out, graph, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(graph);
+  if (ei != hipSuccess) return fail(NLH_ERR_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(ei));
+  return NLH_OK;
+}
+
+// g passes from the current step: the captured graph (captured now if new),
+// ordered after everything enqueued before on every stream, and every later
+// cross-stream wait ordered after it
+int launch_graph(nlh_solver *s, int g, int spp) {
+  nlh_solver::Graph *ge = nullptr;
+  for (auto &x : s->graphs)
+    if (x.passes == g && x.k == s->cur) ge = &x;
+  if (!ge) {
+    nlh_solver::Graph n;
+    n.passes = g;
+    n.k = s->cur;
+    if (int rc = capture_graph(s, g, spp, &n.exec)) return rc;
+    s->graphs.push_back(n);
+    ge = &s->graphs.back();
+  }
+  if (s->exchange) {
+    HIP_TRY(hipStreamWaitEvent(s->s_main, s->ev_halo, 0));  // bands(n-1) and the exchange for halo(n)
+    if (s->sched == 0) HIP_TRY(hipStreamWaitEvent(s->s_main, s->ev_band, 0));
+  }
+  HIP_TRY(hipGraphLaunch(ge->exec, s->s_main));
+  if (s->exchange) {
+    HIP_TRY(hipEventRecord(s->ev_int, s->s_main));
+    HIP_TRY(hipEventRecord(s->ev_band, s->s_main));
+    HIP_TRY(hipEventRecord(s->ev_halo, s->s_main));
+  }
+  if (g & 1) s->cur = 1 - s->cur;
+  s->t += (int64_t)g * spp;
+  if (s->timing) {
+    s->timed_steps += (int64_t)g * spp;
+    s->timed_passes += g;
+  }
+  return NLH_OK;
+}
+
+// wait for a stream by polling it (NLH_SYNC 0): no host-wait flag of the
+// device is needed and the host sees the GPU finish within a query's time.
+// watch: record when the last nlh_run's end event is first seen complete
+// (nlh_host_time).  Past kPollNs the wait blocks in HIP instead, so long runs
+// do not hold a core
+int poll_stream(nlh_solver *s, hipStream_t st, bool watch) {
+  constexpr int64_t kPollNs = 200000000;  // 0.2 s
+  const int64_t t0 = now_ns();
+  watch = watch && s->h_e1 != nullptr && s->h_end_seen < 0;
+  for (;;) {
+    if (watch) {
+      const hipError_t q = hipEventQuery(s->h_e1);
+      if (q == hipSuccess) {
+        s->h_end_seen = now_ns();
+        watch = false;
+      } else if (q != hipErrorNotReady) {
+        return fail(NLH_ERR_HIP, std::string("hipEventQuery: ") + hipGetErrorString(q));
+      }
+    }
+    const hipError_t q = hipStreamQuery(st);
+    if (q == hipSuccess) break;
+    if (q != hipErrorNotReady) return fail(NLH_ERR_HIP, std::string("hipStreamQuery: ") + hipGetErrorString(q));
+    if (now_ns() - t0 > kPollNs) {
+      HIP_TRY(hipStreamSynchronize(st));
+      break;
+    }
+  }
+  if (watch && hipEventQuery(s->h_e1) == hipSuccess) s->h_end_seen = now_ns();
+  return NLH_OK;
+}
+
 // busy milliseconds of each (virtual) rank this process runs since busy
 // timing was enabled (index = rank; ranks run elsewhere stay 0)
 int owner_busy(nlh_solver *s, std::vector<double> &ms) {
@@ -1979,6 +2186,9 @@ int nlh_snapshot_wait(nlh_solver *s, double *u) {
 int nlh_run(nlh_solver *s, int64_t nsteps) {
   if (!s) return fail(NLH_ERR_ARG, "null solver");
   if (nsteps < 0) return fail(NLH_ERR_ARG, "negative step count");
+  s->h_enter = now_ns();
+  s->h_start_seen = s->h_end_seen = -1;
+  s->h_e0 = s->h_e1 = nullptr;
   int rc = set_device(s);
   if (rc) return rc;
   if (nsteps == 0) return NLH_OK;
@@ -1987,19 +2197,45 @@ int nlh_run(nlh_solver *s, int64_t nsteps) {
   // so back-to-back passes are not separated by per-launch event records
   TimedPair run_pair{s};
   const bool per_run = s->timing == 1 || s->timing == 3;
-  if (per_run && (rc = run_pair.begin(s->s_main, kEvRun))) return rc;
+  if (per_run) {
+    if ((rc = run_pair.begin(s->s_main, kEvRun))) return rc;
+    s->h_e0 = s->ev_pool[s->ev_used - 2];
+    s->h_e1 = run_pair.e1;
+  }
   int64_t i = 0;
   // busy and phase timing record 2-4 event pairs per pass: fold the completed
   // ones every kEvFold events inside one long call too, so the pool stays
   // bounded
   auto fold = [&] { return s->timing >= 2 && s->ev_used >= kEvFold ? fold_events(s, false) : (int)NLH_OK; };
-  if (s->pair)
-    for (; i + 2 <= nsteps; i += 2)
-      if ((rc = enqueue_step(s, 2)) || (rc = fold())) return rc;
+  // NLH_HOST_PROBE (diagnostics): after the first pass is enqueued, spin until
+  // the run's start event has completed -- the host time the GPU took to
+  // begin the run (the rest of the passes are enqueued while it runs)
+  auto probe = [&] {
+    if (!s->host_probe || !s->h_e0 || s->h_start_seen >= 0) return (int)NLH_OK;
+    for (;;) {
+      const hipError_t q = hipEventQuery(s->h_e0);
+      if (q == hipSuccess) break;
+      if (q != hipErrorNotReady) return fail(NLH_ERR_HIP, std::string("hipEventQuery: ") + hipGetErrorString(q));
+    }
+    s->h_start_seen = now_ns();
+    return (int)NLH_OK;
+  };
+  const int spp = s->pair ? 2 : 1;
+  while (i + spp <= nsteps) {
+    if (const int g = graph_passes(s, (nsteps - i) / spp)) {
+      if ((rc = launch_graph(s, g, spp)) || (rc = probe())) return rc;
+      i += (int64_t)g * spp;
+      continue;
+    }
+    if ((rc = enqueue_step(s, spp)) || (rc = fold()) || (rc = probe())) return rc;
+    ++s->passes_enqueued;
+    i += spp;
+  }
   for (; i < nsteps; ++i)
-    if ((rc = enqueue_step(s, 1)) || (rc = fold())) return rc;
+    if ((rc = enqueue_step(s, 1)) || (rc = fold()) || (rc = probe())) return rc;
   if (s->exchange) HIP_TRY(hipStreamWaitEvent(s->s_main, s->ev_band, 0));  // last bands
   if (per_run && (rc = run_pair.end(s->s_main))) return rc;
+  s->h_return = now_ns();
   return NLH_OK;
 }
 
@@ -2007,8 +2243,30 @@ int nlh_synchronize(nlh_solver *s) {
   if (!s) return fail(NLH_ERR_ARG, "null solver");
   int rc = set_device(s);
   if (rc) return rc;
-  HIP_TRY(hipStreamSynchronize(s->s_comm));
-  HIP_TRY(hipStreamSynchronize(s->s_main));
+  if (s->sync_mode != 0) {
+    HIP_TRY(hipStreamSynchronize(s->s_comm));
+    HIP_TRY(hipStreamSynchronize(s->s_main));
+  } else {
+    if ((rc = poll_stream(s, s->s_comm, false)) || (rc = poll_stream(s, s->s_main, true))) return rc;
+  }
+  s->h_sync_return = now_ns();
+  return NLH_OK;
+}
+
+int nlh_host_time(nlh_solver *s, nlh_host_times *out) {
+  if (!s || !out) return fail(NLH_ERR_ARG, "null argument");
+  std::memset(out, 0, sizeof(*out));
+  const double e = (double)s->h_enter;
+  out->enqueue_us = (s->h_return - e) / 1e3;
+  out->sync_return_us = s->h_sync_return >= s->h_return ? (s->h_sync_return - e) / 1e3 : -1.0;
+  out->start_seen_us = s->h_start_seen >= 0 ? (s->h_start_seen - e) / 1e3 : -1.0;
+  out->end_seen_us = s->h_end_seen >= 0 ? (s->h_end_seen - e) / 1e3 : -1.0;
+  out->event_span_us = -1.0;
+  if (s->h_e0 && s->h_e1 && hipEventQuery(s->h_e1) == hipSuccess) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, s->h_e0, s->h_e1) == hipSuccess) out->event_span_us = ms * 1e3;
+  }
+  out->sync_mode = s->sync_mode;
   return NLH_OK;
 }
 
@@ -2103,6 +2361,20 @@ int nlh_kernel_timing(nlh_solver *s, int enable) {
   HIP_TRY(hipStreamSynchronize(s->s_band));
   s->timing = (enable == 2 || enable == 3) ? enable : enable != 0 ? 1 : 0;
   s->ev_used = 0;
+  if (s->timing == 1 || s->timing == 3) {
+    // the run pair's two events exist and have been recorded once before the
+    // first timed nlh_run: creating and first recording them inside it
+    // delayed its first launch (r06, tools/host_gap.py: the first timed runs
+    // of a process start their passes 6-9 us later than the rest)
+    while (s->ev_pool.size() < 2) {
+      hipEvent_t e;
+      HIP_TRY(hipEventCreate(&e));
+      s->ev_pool.push_back(e);
+    }
+    HIP_TRY(hipEventRecord(s->ev_pool[0], s->s_main));
+    HIP_TRY(hipEventRecord(s->ev_pool[1], s->s_main));
+    HIP_TRY(hipStreamSynchronize(s->s_main));
+  }
   s->ev_meta.clear();
   for (double &v : s->ev_acc_kind) v = 0.0;
   s->timed_steps = 0;

@@ -151,6 +151,11 @@ int launch_init_test(double *u, int64_t pitch, int32_t bx, int32_t by,
 int launch_fill_w0(double *u, int64_t pitch, int32_t xl, int32_t bx,
                    int32_t by, int32_t halo, int32_t gx0, int32_t gy0, const StepConst &c,
                    void *stream);
+// L_h[W0] (fast test mode, J = 1) from the separable tables StepConst lsx /
+// lty (nlv levels, lty row stride lts) over block-relative x0 .. x0+w,
+// y0 .. y0+h of the plane whose node (0,0) is `out`; 0 outside the lattice.
+int launch_lw_sep(double *out, int64_t pitch, int32_t x0, int32_t y0, int32_t w, int32_t h, int32_t gx0,
+                  int32_t gy0, const StepConst &c, int32_t nlv, int32_t lts, void *stream);
 // Partial L2/Linf per workgroup into `out` (nwg entries); returns nwg.
 int norm_workgroups(int32_t bx, int32_t by);
 int launch_norms(const double *u, int64_t pitch, int32_t bx, int32_t by,

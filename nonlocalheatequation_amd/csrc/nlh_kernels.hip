@@ -461,6 +461,30 @@ __global__ __launch_bounds__(256) void k_fill_w0(double *u, int64_t pitch,
   u[e] = in ? C.sxt[gx + C.E] * C.syt[gy + C.E] : 0.0;
 }
 
+// L_h[W0] of the fast test mode from its separable form (compute_lw, J = 1;
+// the tables of nlh_api.cpp sep_tables, long double on the host, c dh^2 in
+// lsx): per node c dh^2 (sum_l Sx'_l(x) Ty_l(y) + sx(x) Z(y)) -- the
+// reference's sum_local_test disk sum of W0 (:235-252) without its N(eps)
+// sequential roundings, in the operation order of k_pair_split's SEP rows.
+// Over the block-relative rectangle x0 .. x0+w, y0 .. y0+h (the block and the
+// two-step kernel's frame), 0 outside the lattice; one thread per node
+__global__ __launch_bounds__(256) void k_lw_sep(double *out, int64_t pitch, int x0, int y0, int w, int h,
+                                               int gx0, int gy0, StepConst C, int nlv, int lts) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (int64_t)w * h) return;
+  const int x = x0 + (int)(e % w), y = y0 + (int)(e / w);
+  const int gx = gx0 + x, gy = gy0 + y;
+  double a = 0.0;
+  if (gx >= 0 && gx < C.nx && gy >= 0 && gy < C.ny) {
+    const int64_t ncol = pair_sep_ncol(C.E, C.nx);
+    const double *sxp = C.lsx + (gx + 2 * C.E);
+    const double *ty = C.lty + (int64_t)(gy + 2 * C.E) * lts;
+    a = sxp[(int64_t)nlv * ncol] * ty[nlv];
+    for (int l = 0; l < nlv; ++l) a = fma(sxp[(int64_t)l * ncol], ty[l], a);
+  }
+  out[(int64_t)y * pitch + x] = a;
+}
+
 // compute_l2 / compute_linf partials (:96-113)
 __global__ __launch_bounds__(256) void k_norms(const double *u, int64_t pitch,
                                                int bx, int by, int gx0,
@@ -736,6 +760,15 @@ int launch_fill_w0(double *u, int64_t pitch, int32_t xl, int32_t bx, int32_t by,
   const int64_t n = pitch * rows;
   hipLaunchKernelGGL(k_fill_w0, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
                      (hipStream_t)stream, u, pitch, xl, rows, halo, gx0, gy0, c);
+  return check_launch();
+}
+
+int launch_lw_sep(double *out, int64_t pitch, int32_t x0, int32_t y0, int32_t w, int32_t h, int32_t gx0,
+                  int32_t gy0, const StepConst &c, int32_t nlv, int32_t lts, void *stream) {
+  const int64_t n = (int64_t)w * h;
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_lw_sep, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, out, pitch,
+                     x0, y0, w, h, gx0, gy0, c, nlv, lts);
   return check_launch();
 }
 

@@ -301,6 +301,130 @@ double nlh_oracle_time_tiles(const nlh_oracle_params *p, long t, long tiles_x, l
 }
 
 /* ------------------------------------------------------------------------- */
+/* Compensated evaluation (test infrastructure): the same
+ * explicit-Euler step as do_work (:273-303) -- the J = 1 disk sum of
+ * sum_local (:256-270) and the manufactured source of sum_local_test
+ * (:235-252) -- evaluated in x87 long double (64-bit significand) and rounded
+ * to double ONCE per node and step:
+ *   u' = u + dt ( c dh^2 (sum_disk u~_j - N u_i)
+ *                 [ - (2 pi st) w0_i - c dh^2 (sum_disk w~_j - N w_i) ] )
+ * The disk sum of a node is its 2E+1 row windows, row y+dy over columns
+ * x - len(|dy|) .. x + len(|dy|) (the closed lattice disk is symmetric in x
+ * and y, so this is the reference's set of points), each window a difference
+ * of long-double prefix sums of the zero-extended row.  The result is the
+ * reference's arithmetic without the rounding of its N(eps) sequential terms
+ * (at eps >= 64 that rounding, not the GPU kernels', limits the comparison
+ * with nlh_oracle_run): the target of the fast kernels' parity tests at the
+ * stable dt.  J = 1 only (influence 0). */
+typedef struct {
+  const nlh_oracle_params *p;
+  const double *u;
+  double *un;
+  const long double *pu, *pw; /* row prefix sums, (nx + 1) per row */
+  const long *len;            /* len(|d|), d = 0 .. eps */
+  const double *sx_tab, *sy_tab;
+  long double cdh2, st, ct;
+  long y0, y1;
+} comp_job;
+
+static long double window_sum(const long double *prow, long nx, long x, long L) {
+  long a = x - L, b = x + L + 1;
+  if (a < 0) a = 0;
+  if (b > nx) b = nx;
+  return b > a ? prow[b] - prow[a] : 0.0L;
+}
+
+static void *comp_rows(void *arg) {
+  const comp_job *j = (const comp_job *)arg;
+  const long nx = j->p->nx, ny = j->p->ny, eps = j->p->eps;
+  const long double N = (long double)nlh_oracle_disk_count(eps);
+  const long double dt = (long double)j->p->dt;
+  for (long y = j->y0; y < j->y1; ++y)
+    for (long x = 0; x < nx; ++x) {
+      long double su = 0.0L, sw = 0.0L;
+      for (long dy = -eps; dy <= eps; ++dy) {
+        const long yy = y + dy;
+        if (yy < 0 || yy >= ny) continue;
+        const long L = j->len[labs(dy)];
+        su += window_sum(j->pu + yy * (nx + 1), nx, x, L);
+        if (j->p->test) sw += window_sum(j->pw + yy * (nx + 1), nx, x, L);
+      }
+      const long double ui = (long double)j->u[x + y * nx];
+      long double r = j->cdh2 * (su - N * ui);
+      if (j->p->test) {
+        const long double w0 = (long double)j->sx_tab[x + eps] * (long double)j->sy_tab[y + eps];
+        r += -(2.0L * (long double)M_PI * j->st) * w0 - j->cdh2 * (sw - N * (j->ct * w0));
+      }
+      j->un[x + y * nx] = (double)(ui + dt * r);
+    }
+  return NULL;
+}
+
+void nlh_oracle_run_compensated(const nlh_oracle_params *p, long nt, double *u, int nthreads) {
+  const long nx = p->nx, ny = p->ny, eps = p->eps;
+  const size_t n = (size_t)(nx * ny);
+  double *b = (double *)malloc(sizeof(double) * (n ? n : 1));
+  long double *pu = (long double *)malloc(sizeof(long double) * (size_t)(ny * (nx + 1)));
+  long double *pw = p->test ? (long double *)malloc(sizeof(long double) * (size_t)(ny * (nx + 1))) : NULL;
+  long *len = (long *)malloc(sizeof(long) * (size_t)(eps + 1));
+  for (long d = 0; d <= eps; ++d) len[d] = line_len(eps, d);
+  step_ctx c;
+  ctx_init(&c, p);
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > ny) nthreads = ny > 0 ? (int)ny : 1;
+  pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)nthreads);
+  comp_job *jobs = (comp_job *)malloc(sizeof(comp_job) * (size_t)nthreads);
+  double *cur = u, *nxt = b;
+  for (long t = 0; t < nt; ++t) {
+    ctx_time(&c, t);
+    for (long y = 0; y < ny; ++y) {
+      long double *r = pu + y * (nx + 1);
+      long double *q = pw ? pw + y * (nx + 1) : NULL;
+      r[0] = 0.0L;
+      if (q) q[0] = 0.0L;
+      for (long x = 0; x < nx; ++x) {
+        r[x + 1] = r[x] + (long double)cur[x + y * nx];
+        if (q)
+          q[x + 1] = q[x] + (long double)c.ct * (long double)c.sx_tab[x + eps] * (long double)c.sy_tab[y + eps];
+      }
+    }
+    for (int i = 0; i < nthreads; ++i) {
+      comp_job *j = &jobs[i];
+      j->p = p;
+      j->u = cur;
+      j->un = nxt;
+      j->pu = pu;
+      j->pw = pw;
+      j->len = len;
+      j->sx_tab = c.sx_tab;
+      j->sy_tab = c.sy_tab;
+      j->cdh2 = (long double)c.c2d * (long double)c.dh2;
+      j->st = (long double)c.st;
+      j->ct = (long double)c.ct;
+      j->y0 = ny * i / nthreads;
+      j->y1 = ny * (i + 1) / nthreads;
+      if (nthreads > 1)
+        pthread_create(&th[i], NULL, comp_rows, j);
+      else
+        comp_rows(j);
+    }
+    if (nthreads > 1)
+      for (int i = 0; i < nthreads; ++i) pthread_join(th[i], NULL);
+    double *tmp = cur;
+    cur = nxt;
+    nxt = tmp;
+  }
+  if (cur != u) memcpy(u, cur, sizeof(double) * n);
+  ctx_free(&c);
+  free(jobs);
+  free(th);
+  free(len);
+  free(pw);
+  free(pu);
+  free(b);
+}
+
+/* ------------------------------------------------------------------------- */
 /* 1D solver (src/1d_nonlocal_serial.cpp)                                      */
 double nlh_oracle_c1d(long eps, double k, double dx) {
   const long c = (long)((k * 3) / (pow(eps * dx, 3))); /* `long c_1d` (1d :57,74) */

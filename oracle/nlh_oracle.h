@@ -63,6 +63,10 @@ void nlh_oracle_step(const nlh_oracle_params *p, long t, const double *u,
 /* nt steps starting from u (overwritten with the state at time nt).        */
 void nlh_oracle_run(const nlh_oracle_params *p, long nt, double *u,
                     int nthreads);
+/* The same steps evaluated in long double and rounded once per node and step
+ * (J = 1): the fast kernels' target at the stable dt, free of the
+ * reference's sequential-sum rounding (nlh_oracle.c). */
+void nlh_oracle_run_compensated(const nlh_oracle_params *p, long nt, double *u, int nthreads);
 
 /* compute_l2 / compute_linf at `time` (:96-113): l2 = sum (u-w)^2 accumulated
  * sx-outer / sy-inner, no sqrt;  linf = max |u-w|                           */

@@ -56,6 +56,7 @@ def lib() -> ctypes.CDLL:
         L.nlh_oracle_step.argtypes = [P, ctypes.c_long, dp, dp, ctypes.c_int]
         L.nlh_oracle_run.argtypes = [P, ctypes.c_long, dp, ctypes.c_int]
         L.nlh_oracle_errors.argtypes = [P, ctypes.c_long, dp, dp, dp]
+        L.nlh_oracle_run_compensated.argtypes = [P, ctypes.c_long, dp, ctypes.c_int]
         L.nlh_oracle_run_tiled.argtypes = [P, ctypes.c_long, ctypes.c_long, ctypes.c_long, dp, ctypes.c_int]
         L.nlh_oracle_run_tiled.restype = ctypes.c_double
         L.nlh_oracle_time_tiles.argtypes = [P, ctypes.c_long, ctypes.c_long, ctypes.c_long, ctypes.c_long,
@@ -116,6 +117,17 @@ def step(p: Params, t: int, u: np.ndarray, nthreads: int | None = None) -> np.nd
 def run(p: Params, nt: int, u: np.ndarray | None = None, nthreads: int | None = None) -> np.ndarray:
     u = test_init(p) if u is None else np.array(u, dtype=np.float64, order="C", copy=True)
     lib().nlh_oracle_run(ctypes.byref(p), int(nt), _dp(u), nthreads or default_threads())
+    return u
+
+
+def run_compensated(p: Params, nt: int, u: np.ndarray | None = None, nthreads: int | None = None) -> np.ndarray:
+    """The same steps in long double, rounded to double once per node and step
+    (J = 1): the reference's arithmetic without the rounding of its N(eps)
+    sequential terms (nlh_oracle.c nlh_oracle_run_compensated)."""
+    if p.influence != 0:
+        raise ValueError("run_compensated: J = 1 only")
+    u = test_init(p) if u is None else np.array(u, dtype=np.float64, order="C", copy=True)
+    lib().nlh_oracle_run_compensated(ctypes.byref(p), int(nt), _dp(u), nthreads or default_threads())
     return u
 
 

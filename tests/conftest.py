@@ -153,9 +153,14 @@ def check_nodes(u, u_ref, what: str = "", scale=None, tol: float = 1e-12) -> dic
     relative error (node_errors) recorded beside it, before the assertion, to
     gpurun_out/parity_nodes.jsonl."""
     import json
+    import numpy as np
     st = node_errors(u, u_ref, scale)
     rec = {"test": os.environ.get("PYTEST_CURRENT_TEST", "").split(" ")[0], "what": what,
            "n": int(getattr(u_ref, "size", 0)), "tol_field_scale": tol, **st}
+    if scale is not None:  # the scale given (e.g. the run's largest field): the final field's beside it
+        fin = float(np.max(np.abs(u_ref)))
+        rec["final_field_scale"] = fin
+        rec["max_abs_diff_over_final_scale"] = st["max_abs_diff"] / fin if fin > 0 else None
     try:
         with open(os.path.join(_record_dir(), "parity_nodes.jsonl"), "a") as f:
             f.write(json.dumps(rec) + "\n")

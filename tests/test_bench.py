@@ -159,3 +159,49 @@ def test_read_tile_map_reference_c5():
     for i in range(25):
         px, py, o = vals[3 * i:3 * i + 3]
         assert own[px + py * npx] == o
+
+
+def test_roofline_fields_two_step_pass():
+    """a two-step pass must move u^t once and u^{t+2} once,
+    16 B per node and launch -- 268.4 MB at C2 -- so frac = 268.4 MB / launch
+    time / 8 TB/s and never exceeds 1 for a physically possible launch; the
+    16-B-per-node-update figure is the separate `effective_*` key."""
+    nodes = 4096 * 4096
+    t = 67.60e-6  # rocprofv3 mean of k_pair_split at C2 (profiles/r05/evidence/c2)
+    r = bench.roofline_fields(nodes, 2, t, 197, False)
+    assert r["algorithmic_bytes_per_launch"] == 16 * nodes == 268_435_456
+    assert r["node_updates_per_launch"] == 2 * nodes
+    assert abs(r["achieved"] - 268_435_456 / t / 1e9) < 1e-6
+    assert abs(r["frac"] - 0.4964) < 1e-3 and r["frac"] <= 1.0
+    assert abs(r["effective_frac"] - 2 * r["frac"]) < 1e-12
+    assert r["algorithmic_bytes_per_node_update"] == 8.0
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == bench.HBM_PEAK_GBS
+    # the bound follows the PMC limiter when there is one
+    assert bench.roofline_fields(nodes, 2, t, 197, False, {"limiter": "fp64_valu_issue"})["bound"] == "fp64_valu"
+    # the fastest launch HBM allows moves exactly the algorithmic bytes at peak: frac 1
+    fastest = 16 * nodes / (bench.HBM_PEAK_GBS * 1e9)
+    assert abs(bench.roofline_fields(nodes, 2, fastest, 197, False)["frac"] - 1.0) < 1e-12
+    # test mode: the L_h[W0] plane once per pass; single-step kernels: 16 (+8) B per node-update
+    rt = bench.roofline_fields(nodes, 2, t, 197, True)
+    assert rt["algorithmic_bytes_per_launch"] == 24 * nodes
+    r1 = bench.roofline_fields(nodes, 1, t, 197, True)
+    assert r1["algorithmic_bytes_per_node_update"] == 24.0 and r1["effective_bytes_per_launch"] == 24 * nodes
+
+
+def test_watchdog_quiet_stage_does_not_wake(monkeypatch):
+    """The timed stage moves the watchdog's deadline without waking its
+    thread (no thread start or wake-up inside the timed region), and a stage
+    still expires at its deadline."""
+    monkeypatch.delenv("NLH_BENCH_STAGE_TIMEOUT", raising=False)
+    st = bench.Stages(0, 1)
+    st.enter("warmup")
+    wakes = []
+    orig = st.cv.notify
+    st.cv.notify = lambda *a: (wakes.append(1), orig(*a))
+    st.enter("timed", quiet=True)
+    assert wakes == [] and st.name == "timed"
+    st.enter("report")
+    assert wakes == [1]
+    st.end()
+    st.thread.join(5)
+    assert not st.thread.is_alive()

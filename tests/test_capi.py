@@ -37,7 +37,7 @@ def test_python_binding_covers_header():
 
 
 def test_abi_version():
-    assert N.lib().nlh_abi_version() == 9
+    assert N.lib().nlh_abi_version() == 10
 
 
 def test_build_id_matches_sources():
@@ -82,14 +82,16 @@ def test_params_layout_matches_header():
                 ' offsetof(nlh_params, tiles_x), offsetof(nlh_params, comm_id),'
                 ' sizeof(nlh_info), offsetof(nlh_info, arch), offsetof(nlh_info, steps_per_pass));'
                 ' printf("%zu %zu %zu %zu\\n", offsetof(nlh_info, comm_nranks), offsetof(nlh_info, comm_rank),'
-                ' sizeof(nlh_phase_times), offsetof(nlh_phase_times, passes)); return 0;}\n')
+                ' sizeof(nlh_phase_times), offsetof(nlh_phase_times, passes));'
+                ' printf("%zu %zu\\n", sizeof(nlh_host_times), offsetof(nlh_host_times, sync_mode)); return 0;}\n')
     exe = os.path.join(ROOT, "build", "probe_layout")
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), src, "-o", exe], check=True)
     vals = list(map(int, subprocess.run([exe], capture_output=True, text=True, check=True).stdout.split()))
     assert vals == [ctypes.sizeof(N._Params), N._Params.tiles_x.offset, N._Params.comm_id.offset,  # noqa: SLF001
                     ctypes.sizeof(N._Info), N._Info.arch.offset, N._Info.steps_per_pass.offset,  # noqa: SLF001
                     N._Info.comm_nranks.offset, N._Info.comm_rank.offset,  # noqa: SLF001
-                    ctypes.sizeof(N._PhaseTimes), N._PhaseTimes.passes.offset]  # noqa: SLF001
+                    ctypes.sizeof(N._PhaseTimes), N._PhaseTimes.passes.offset,  # noqa: SLF001
+                    ctypes.sizeof(N._HostTimes), N._HostTimes.sync_mode.offset]  # noqa: SLF001
 
 
 @pytest.mark.skipif(gpu_available(), reason="checks the no-GPU failure path")

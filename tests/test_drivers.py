@@ -172,3 +172,27 @@ def test_serial_driver_large_horizon(oracle, eps):
     l2, li = oracle.errors(p, nt, oracle.run(p, nt))
     m = re.search(r"^l2: (\S+) linfinity: (\S+)$", out, re.M)
     assert m and float(m.group(1)) == pytest.approx(l2, rel=1e-5) and float(m.group(2)) == pytest.approx(li, rel=1e-5)
+
+
+def test_auto_kernel_choice_and_note(oracle):
+    """--kernel auto in test mode runs EXACT where the whole
+    run is cheap (nx*ny*nt*N(eps) <= 2e11 disk terms), so the printed l2 /
+    linfinity are the reference's own order -- bit for bit with the oracle --
+    and says nothing; past that it runs a FAST kernel and one stderr line
+    names the kernel and the L2 contract."""
+    p = subprocess.run([os.path.join(BIN, "2d_nonlocal_serial"), "--test", "--cmp", "false", "--nx", "120",
+                        "--ny", "100", "--nt", "30", "--eps", "8", "--dh", repr(1 / 120), "--dt", "1e-6",
+                        "--nlog", "1000"], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0 and "note:" not in p.stderr, p.stderr
+    o = oracle.params(120, 100, 8, 1.0, 1e-6, 1 / 120, 1)
+    l2, li = oracle.errors(o, 30, oracle.run(o, 30))
+    assert p.stdout.splitlines()[1] == f"l2: {l2:g} linfinity: {li:g}"
+    n = 1200  # 1200^2 * 800 * 197 = 2.3e11 terms: FAST
+    p = subprocess.run([os.path.join(BIN, "2d_nonlocal_serial"), "--test", "--cmp", "false", "--nx", str(n),
+                        "--ny", str(n), "--nt", "800", "--eps", "8", "--dh", repr(1 / n),
+                        "--dt", repr(8 ** 4 / (n * n * 8 * 197)), "--nlog", "100000"],
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr
+    notes = [l for l in p.stderr.splitlines() if l.startswith("note: --kernel auto ran the FAST kernel")]
+    assert len(notes) == 1 and "k_pair_split" in notes[0] and "--kernel exact" in notes[0], p.stderr
+    assert p.stdout.splitlines()[1].startswith("l2: ")

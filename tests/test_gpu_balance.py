@@ -332,6 +332,29 @@ def test_driver_nbalance_virtual_ranks(oracle, tmp_path):
     assert m and float(m.group(1)) == pytest.approx(l2, rel=1e-5) and float(m.group(2)) == pytest.approx(li, rel=1e-5)
 
 
+@pytest.mark.parametrize("nbal", [1, 3, 10])
+def test_driver_nbalance_busy_window(oracle, tmp_path, nbal):
+    """--nbalance WITHOUT --test_load_balance: busy timing runs only
+    in a window of at most nbalance steps before each balance point (the rest
+    of each interval keeps the overlapped exchange schedule).  --nbalance 1
+    used to leave the window closed after the first balance and die in the
+    second nlh_rebalance ('busy timing is off'); every interval length must
+    run through, and the field through the repartitions stays the oracle's."""
+    f, npx, npy, own, R = _scaled_map(tmp_path, "load_balance_25s_4n.txt", 32)
+    env = dict(os.environ, NLH_VIRTUAL_RANKS=str(R))
+    nt, dt = 12, 3e-5
+    out = subprocess.run([os.path.join(ROOT, "bin", "2d_nonlocal_distributed"), "--file", str(f),
+                          "--nt", str(nt), "--dt", str(dt), "--eps", "5", "--nbalance", str(nbal),
+                          "--nlog", "1000"],
+                         capture_output=True, text=True, timeout=300, env=env)
+    assert out.returncode == 0, out.stderr
+    n = 32 * npx
+    p = oracle.params(n, n, 5, 1.0, dt, 1.0 / n, 1)
+    l2, li = oracle.errors(p, nt, oracle.run(p, nt))
+    m = re.search(r"^l2: (\S+) linfinity: (\S+)$", out.stdout, re.M)
+    assert m and float(m.group(1)) == pytest.approx(l2, rel=1e-5) and float(m.group(2)) == pytest.approx(li, rel=1e-5)
+
+
 def test_driver_balances_large_tiles(tmp_path):
     """The same map with 2048^2 tiles (10240^2 lattice): busy time is kernel
     work, so after the --nbalance rounds the reference's verdict (:682-685:

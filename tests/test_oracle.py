@@ -198,3 +198,58 @@ def test_oracle_1d_restatement_small(oracle):
             nxt[x] += r2 * dt
     u = oracle.run_1d(nx, nt, eps, k, dt, dx, True)
     assert u.tolist() == S[nt % 2]
+
+
+def _direct_longdouble_step(oracle, p, u0):
+    """One step by the disk loops themselves in numpy long double (x87 80-bit
+    here and on the GPU box), rounded once: the compensated oracle's spec."""
+    import math
+    L = np.longdouble
+    nx, ny, eps = p.nx, p.ny, p.eps
+    c, dh2, dt = L(oracle.c2d(p)), L(p.dh * p.dh), L(p.dt)
+    st, ct = L(math.sin(2 * math.pi * (0 * p.dt))), L(math.cos(2 * math.pi * (0 * p.dt)))
+    sx = [L(math.sin(2 * math.pi * (i * p.dh))) for i in range(nx)]
+    sy = [L(math.sin(2 * math.pi * (i * p.dh))) for i in range(ny)]
+    n = oracle.disk_count(eps)
+    out = np.zeros((ny, nx))
+    for y in range(ny):
+        for x in range(nx):
+            su = sw = L(0)
+            for dx in range(-eps, eps + 1):  # sx outer, as the reference
+                ln = int(math.sqrt(eps * eps - dx * dx))
+                for dy in range(-ln, ln + 1):
+                    xx, yy = x + dx, y + dy
+                    if 0 <= xx < nx and 0 <= yy < ny:
+                        su += L(u0[yy, xx])
+                        sw += ct * sx[xx] * sy[yy]
+            ui = L(u0[y, x])
+            r = c * dh2 * (su - n * ui)
+            if p.test:
+                w0 = sx[x] * sy[y]
+                r += -(2 * L(math.pi) * st) * w0 - c * dh2 * (sw - n * (ct * w0))
+            out[y, x] = float(ui + dt * r)
+    return out
+
+
+@pytest.mark.parametrize("test", [0, 1])
+def test_compensated_oracle_is_the_longdouble_disk_sum(oracle, test):
+    """oracle.run_compensated (row windows of long-double
+    prefix sums) equals the disk loops evaluated in long double, rounded once
+    -- bit for bit on a ragged lattice whose disk leaves the domain."""
+    eps, nx, ny = 7, 23, 19
+    dh = 1.0 / nx
+    p = oracle.params(nx, ny, eps, 1.0, 0.3 * eps ** 4 * dh * dh / (8 * oracle.disk_count(eps)), dh, test)
+    u0 = np.random.default_rng(1).uniform(-1, 1, (ny, nx))
+    assert np.array_equal(oracle.run_compensated(p, 1, u0), _direct_longdouble_step(oracle, p, u0))
+
+
+@pytest.mark.parametrize("eps,test", [(3, 1), (5, 1), (8, 0), (8, 1), (12, 1)])
+def test_compensated_oracle_near_reference_order(oracle, eps, test):
+    """Where the reference's N(eps) sequential terms round little (small eps),
+    the compensated steps stay within a few ulp of field scale of the
+    reference's own order over several steps at the stable dt (alpha N = 1)."""
+    nx, ny = 50, 43
+    dh = 1.0 / nx
+    p = oracle.params(nx, ny, eps, 1.0, eps ** 4 * dh * dh / (8 * oracle.disk_count(eps)), dh, test)
+    a, b = oracle.run(p, 5), oracle.run_compensated(p, 5)
+    assert np.abs(a - b).max() <= 1e-14 * np.abs(a).max()

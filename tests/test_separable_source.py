@@ -1,6 +1,7 @@
 """The separable form of the manufactured source's operator term, as the
-two-step test-mode pass uses it (nlh_pair.h OPT & 32768, nlh_api.cpp
-sep_tables): with the reference's zero-extended W0 = sx(x) sy(y)
+fast test mode's L_h[W0] plane is computed from it (round 6: nlh_api.cpp
+sep_tables + compute_lw, k_lw_sep; also nlh_pair.h OPT & 32768, harness
+only): with the reference's zero-extended W0 = sx(x) sy(y)
 (sum_local_test, src/2d_nonlocal_serial.cpp:235-252),
 
     L_h[W0](x, y) = c dh^2 (sum_l Sx'_l(x) Ty_l(y) + sx(x) Z(y)),
