@@ -1560,7 +1560,11 @@ int repartition_fits(nlh_solver *s, const std::vector<int32_t> &own) {
   }
   const int64_t tile_bytes = (s->p.nx / s->p.tiles_x) * (s->p.ny / s->p.tiles_y) * (int64_t)sizeof(double);
   const double scale = tiles_old > 0 ? (double)tiles_new / (double)tiles_old : 1.0;
-  const double need = (double)s->device_bytes * scale * 1.05 + (double)(moving * tile_bytes) + 64.0 * (1 << 20);
+  // staging: the kept buffer (stage_cap, already allocated, so not in the free
+  // memory) covers that much of the moving tiles; repartition_impl frees it
+  // before allocating a larger one (round 5 counted it twice)
+  const double stage_new = std::max(0.0, (double)(moving * tile_bytes) - (double)s->stage_cap * sizeof(double));
+  const double need = (double)s->device_bytes * scale * 1.05 + stage_new + 64.0 * (1 << 20);
   size_t free_b = 0, total_b = 0;
   // a local failure votes "does not fit" but still joins the all-reduce below:
   // returning early here would leave the other ranks waiting in it

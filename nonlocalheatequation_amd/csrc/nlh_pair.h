@@ -943,7 +943,11 @@ template <int E>
 int pair_blocks_per_cu_e(int variant) {
   int n = 0;
   hipError_t e = hipErrorInvalidValue;
-  variant &= ~kPairNoPrio;  // same resources with or without the priority
+  // the priority variant's residency: the host launches a list with the
+  // priority only when all its workgroups are resident at once in THAT
+  // variant (the no-priority one, without the period-aligned rings, holds
+  // less LDS and may fit more per CU; that count decides nothing)
+  variant &= ~kPairNoPrio;
   if (variant == 1) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_pair_split<E, kPairSplitD>, 128, 0);
   else if (variant == 6) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_pair_split<E, 4, 0, 2>, 128, 0);
   else if (variant == 5)

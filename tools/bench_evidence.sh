@@ -12,6 +12,8 @@ export TMPDIR=/tmp
 timeout -k 10 300 python bench.py "$@" > "$O/bench.json" 2> "$O/bench.err" || exit 1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run --output-format csv -- python3 bench.py --no-cpu-baseline "$@" > "$O/bench_prof.json" 2> "$O/bench_prof.err" || exit 1
 tools/pmc.sh "$O/pmc" python3 tools/prof_step.py > "$O/pmc.log" 2>&1 || exit 1
+# the per-launch trace is large; the --stats summary is the committed record
+rm -f "$O"/prof/*kernel_trace.csv
 BID=$(python3 -c "import sys; sys.path.insert(0, '.'); import nonlocalheatequation_amd as N; print(N.build_id())")
 python3 tools/pmc_summary.py "$O/pmc" "$KERNEL" --workload "$WKEY" --node-updates "$NU" --commit "$COMMIT" --build-id "$BID" > "$O/pmc_record.json" || exit 1
 echo "done $WKEY"
