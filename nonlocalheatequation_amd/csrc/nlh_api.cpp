@@ -17,8 +17,12 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <execinfo.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <atomic>
+#include <csignal>
 #include <chrono>
 #include <cmath>
 #include <condition_variable>
@@ -174,10 +178,32 @@ constexpr EnvKnob kEnvKnobs[] = {
                                    // host-wait flag (yield, blocking, auto, spin) and block in HIP
     {"NLH_HOST_PROBE", 0, 1},      // diagnostics: nlh_run spins until its first launch has started
     {"NLH_GRAPH", 0, 1},           // 1: production passes replayed from captured HIP graphs
+    {"NLH_SEGV_TRACE", 0, 1},      // diagnostics: a native backtrace on stderr on SIGSEGV / SIGBUS
     {"NLH_PAIR_PRIO", 0, 2},       // k_pair_split wave priority: 0 never, 1 one-round lists (default), 2 not on bands
     {"NLH_TRACE_REPART", 0, 1},    // repartition phase times on stderr
 };
 constexpr const char *kRemovedKnobs[] = {"NLH_ABLATE", "NLH_PAIR_ABLATE"};
+
+// NLH_SEGV_TRACE=1 (diagnostics): a native backtrace on stderr when the
+// process takes SIGSEGV / SIGBUS, then the default action (a Python
+// faulthandler shows only the interpreter's frames)
+void segv_trace(int sig) {
+  void *f[64];
+  const int n = backtrace(f, 64);
+  const char msg[] = "libnlh NLH_SEGV_TRACE: fatal signal, native backtrace:\n";
+  (void)!write(2, msg, sizeof msg - 1);
+  backtrace_symbols_fd(f, n, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+
+void install_segv_trace() {
+  static std::once_flag once;
+  std::call_once(once, [] {
+    signal(SIGSEGV, segv_trace);
+    signal(SIGBUS, segv_trace);
+  });
+}
 
 int check_env() {
   for (const char *name : kRemovedKnobs)
@@ -379,6 +405,10 @@ struct nlh_solver {
   int64_t passes_enqueued = 0;  // ungraphed passes since creation (RCCL peers connected before capture)
   bool capture_first = false;   // capturing the graph's first pass: no waits on events recorded outside it
   hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_join2 = nullptr;
+  // the schedule's cross-stream events while a graph is captured (capture_graph
+  // swaps them in: an event recorded inside a capture is never waited on
+  // outside it, nor one recorded outside inside it)
+  hipEvent_t evc_ready = nullptr, evc_halo = nullptr, evc_band = nullptr, evc_int = nullptr;
 };
 
 namespace {
@@ -1031,6 +1061,8 @@ void release_impl(nlh_solver *s, bool keep_comm) {
   trace_mark("r_sync");
   for (auto &g : s->graphs) (void)hipGraphExecDestroy(g.exec);
   s->graphs.clear();
+  for (hipEvent_t e : {s->evc_ready, s->evc_halo, s->evc_band, s->evc_int})
+    if (e) (void)hipEventDestroy(e);
   if (s->ev_fork) (void)hipEventDestroy(s->ev_fork);
   if (s->ev_join) (void)hipEventDestroy(s->ev_join);
   if (s->ev_join2) (void)hipEventDestroy(s->ev_join2);
@@ -1217,6 +1249,8 @@ int create_impl(const nlh_params *pin, nlh_solver *s, ncclComm_t reuse_comm = nu
   }
   if (const char *v = std::getenv("NLH_HOST_PROBE")) s->host_probe = *v && std::atoi(v) != 0;
   if (const char *v = std::getenv("NLH_GRAPH")) s->graph_on = *v && std::atoi(v) != 0;
+  if (const char *v = std::getenv("NLH_SEGV_TRACE"))
+    if (*v && std::atoi(v) != 0) install_segv_trace();
   hipDeviceProp_t prop;
   HIP_TRY(hipGetDeviceProperties(&prop, s->device));
   std::snprintf(s->arch, sizeof(s->arch), "%s", prop.gcnArchName);
@@ -1843,14 +1877,23 @@ int graph_passes(const nlh_solver *s, int64_t passes_left) {
 
 int capture_graph(nlh_solver *s, int g, int spp, hipGraphExec_t *out) {
   if (s->exchange && !s->ev_fork) {
-    HIP_TRY(hipEventCreateWithFlags(&s->ev_fork, hipEventDisableTiming));
-    HIP_TRY(hipEventCreateWithFlags(&s->ev_join, hipEventDisableTiming));
-    HIP_TRY(hipEventCreateWithFlags(&s->ev_join2, hipEventDisableTiming));
+    for (hipEvent_t *e : {&s->ev_fork, &s->ev_join, &s->ev_join2, &s->evc_ready, &s->evc_halo, &s->evc_band,
+                          &s->evc_int})
+      HIP_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming));
   }
+  // the capture records and waits on its own events, never on the ones the
+  // ungraphed schedule records outside it
+  auto swap_events = [s] {
+    std::swap(s->ev_ready, s->evc_ready);
+    std::swap(s->ev_halo, s->evc_halo);
+    std::swap(s->ev_band, s->evc_band);
+    std::swap(s->ev_int, s->evc_int);
+  };
   const int64_t t0 = s->t, steps0 = s->timed_steps, passes0 = s->timed_passes;
   const int cur0 = s->cur;
   const bool band_stream = s->exchange && s->sched == 0;
   HIP_TRY(hipStreamBeginCapture(s->s_main, hipStreamCaptureModeRelaxed));
+  if (s->exchange) swap_events();
   int rc = NLH_OK;
   auto body = [&]() -> int {
     if (s->exchange) {
@@ -1877,6 +1920,7 @@ int capture_graph(nlh_solver *s, int g, int spp, hipGraphExec_t *out) {
   rc = body();
   hipGraph_t graph = nullptr;
   const hipError_t ec = hipStreamEndCapture(s->s_main, &graph);
+  if (s->exchange) swap_events();
   s->t = t0;
   s->cur = cur0;
   s->timed_steps = steps0;
