@@ -1857,19 +1857,24 @@ int fold_events(nlh_solver *s, bool drain) {
 // ---- HIP graphs of production passes (NLH_GRAPH=1)
 // A run of g passes is captured once per (g, start parity) and replayed with
 // one hipGraphLaunch on s_main: the pass launches, and with an exchange every
-// pass's interior / bands / pack / grouped ncclSend-ncclRecv / unpack on the
-// streams and with the cross-stream events of the ungraphed schedule (the
-// side streams fork from s_main at the start and join it at the end), so the
-// host enqueues one launch per g passes instead of each pass's kernels,
-// events and RCCL calls.  The kernels and their arguments are the ungraphed
-// ones: bitwise equal fields.  Production mode only (test mode's per-step
-// source constants are kernel arguments), kernel timing 0 / 1 only, and only
-// once the halo is fresh and an ungraphed exchange has connected RCCL's peers.
+// pass's interior / bands / pack / unpack / local block copies on the streams
+// and with the cross-stream order of the ungraphed schedule (the side
+// streams fork from s_main at the start and join it at the end).  The
+// kernels and their arguments are the ungraphed ones: bitwise equal fields.
+// Production mode only (test mode's per-step source constants are kernel
+// arguments), kernel timing 0 / 1 only, once the halo is fresh -- and only
+// for solvers without RCCL messages: with grouped ncclSend / ncclRecv inside
+// the capture the process died in nlh_run (SIGSEGV) in 2 of 3 whole-suite
+// runs on MI355X (RCCL 2.27.7, send/recv to self; the same test alone, and
+// the suite under pytest -s, passed), and on ROCm 7.2 a graph launch costs
+// the host about what its nodes' direct launches cost with an exchange
+// (per pass 86 -> 73 us for C3's 8 virtual ranks, profiles/r06/graph), so
+// graphs stay an option, off by default.
 constexpr int kGraphMaxPasses = 16;
 
 int graph_passes(const nlh_solver *s, int64_t passes_left) {
   if (!s->graph_on || s->p.test || (s->timing != 0 && s->timing != 1)) return 0;
-  if (s->exchange && (!s->halo_fresh || s->passes_enqueued < 2)) return 0;
+  if (s->exchange && (!s->halo_fresh || s->passes_enqueued < 2 || !s->peers.empty())) return 0;
   int g = 0;
   for (int c = 2; c <= kGraphMaxPasses && c <= passes_left; c *= 2) g = c;
   return g;
