@@ -393,22 +393,16 @@ struct nlh_solver {
   bool host_probe = false;  // NLH_HOST_PROBE: record when the run's start event completes
   int64_t h_enter = 0, h_return = 0, h_start_seen = -1, h_end_seen = -1, h_sync_return = 0;
   hipEvent_t h_e0 = nullptr, h_e1 = nullptr;  // the last nlh_run's event pair (timing 1 / 3)
-  // HIP graphs of production passes (NLH_GRAPH=1): runs of g passes (g a
-  // power of two, 2 .. kGraphMaxPasses) starting at buffer parity k, captured
-  // on first use and replayed by one hipGraphLaunch each (capture_graph)
+  // HIP graphs of production passes (NLH_GRAPH=1, single-stream solvers):
+  // runs of g passes (g a power of two, 2 .. kGraphMaxPasses) starting at
+  // buffer parity k, captured on first use and replayed by one hipGraphLaunch
+  // each (capture_graph)
   struct Graph {
     int passes = 0, k = 0;
     hipGraphExec_t exec = nullptr;
   };
   bool graph_on = false;
   std::vector<Graph> graphs;
-  int64_t passes_enqueued = 0;  // ungraphed passes since creation (RCCL peers connected before capture)
-  bool capture_first = false;   // capturing the graph's first pass: no waits on events recorded outside it
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_join2 = nullptr;
-  // the schedule's cross-stream events while a graph is captured (capture_graph
-  // swaps them in: an event recorded inside a capture is never waited on
-  // outside it, nor one recorded outside inside it)
-  hipEvent_t evc_ready = nullptr, evc_halo = nullptr, evc_band = nullptr, evc_int = nullptr;
 };
 
 namespace {
@@ -918,10 +912,6 @@ int enqueue_step(nlh_solver *s, int nsteps) {
       if ((rc = enqueue_exchange(s, k))) return rc;
       s->halo_fresh = true;
     }
-    // a graph's first pass: the launch itself is ordered after every
-    // earlier pass on all streams (launch_graph), and events recorded outside
-    // the capture cannot be waited on inside it
-    const bool outside = !s->capture_first;
     if (s->timing == 2) {
       // busy timing: the pass serialised on s_main -- halo(n), every rank's
       // bands, every rank's interior -- so each rank's pairs time its own
@@ -936,7 +926,7 @@ int enqueue_step(nlh_solver *s, int nsteps) {
     } else if (s->sched == 1) {
       // bands(n) then interior(n), both on s_main: the bands run alone
       // briefly and the interior keeps its one-round grid
-      if (outside) HIP_TRY(hipStreamWaitEvent(s->s_main, s->ev_halo, 0));  // halo(n)
+      HIP_TRY(hipStreamWaitEvent(s->s_main, s->ev_halo, 0));  // halo(n)
       if ((rc = stencil(s->rl_bnd[k], s->pl_bnd[k], s->s_main, kEvBand))) return rc;
       HIP_TRY(hipEventRecord(s->ev_band, s->s_main));
       if ((rc = stencil(s->rl_int[k], s->pl_int[k], s->s_main, kEvInterior))) return rc;
@@ -946,10 +936,8 @@ int enqueue_step(nlh_solver *s, int nsteps) {
       // the chain bands -> pack -> send/recv -> unpack -> next bands crosses
       // no queue; only interior(n-1) -> bands(n) and bands(n-1) -> interior(n)
       // do (about 11 us per cross-queue wait, profiles/r01/sched)
-      if (outside) {
-        HIP_TRY(hipStreamWaitEvent(s->s_main, s->ev_band, 0));  // bands(n-1)
-        HIP_TRY(hipStreamWaitEvent(s->s_comm, s->ev_int, 0));   // interior(n-1)
-      }
+      HIP_TRY(hipStreamWaitEvent(s->s_main, s->ev_band, 0));  // bands(n-1)
+      HIP_TRY(hipStreamWaitEvent(s->s_comm, s->ev_int, 0));   // interior(n-1)
       if ((rc = stencil(s->rl_int[k], s->pl_int[k], s->s_main, kEvInterior))) return rc;
       HIP_TRY(hipEventRecord(s->ev_int, s->s_main));
       if ((rc = stencil(s->rl_bnd[k], s->pl_bnd[k], s->s_comm, kEvBand))) return rc;
@@ -959,11 +947,9 @@ int enqueue_step(nlh_solver *s, int nsteps) {
       s->t += nsteps;
       return NLH_OK;
     } else {
-      if (outside) {
-        HIP_TRY(hipStreamWaitEvent(s->s_main, s->ev_band, 0));  // bands(n-1)
-        HIP_TRY(hipStreamWaitEvent(s->s_band, s->ev_int, 0));   // interior(n-1)
-        HIP_TRY(hipStreamWaitEvent(s->s_band, s->ev_halo, 0));  // halo(n)
-      }
+      HIP_TRY(hipStreamWaitEvent(s->s_main, s->ev_band, 0));  // bands(n-1)
+      HIP_TRY(hipStreamWaitEvent(s->s_band, s->ev_int, 0));   // interior(n-1)
+      HIP_TRY(hipStreamWaitEvent(s->s_band, s->ev_halo, 0));  // halo(n)
       if ((rc = stencil(s->rl_int[k], s->pl_int[k], s->s_main, kEvInterior))) return rc;
       HIP_TRY(hipEventRecord(s->ev_int, s->s_main));
       if ((rc = stencil(s->rl_bnd[k], s->pl_bnd[k], s->s_band, kEvBand))) return rc;
@@ -1061,11 +1047,6 @@ void release_impl(nlh_solver *s, bool keep_comm) {
   trace_mark("r_sync");
   for (auto &g : s->graphs) (void)hipGraphExecDestroy(g.exec);
   s->graphs.clear();
-  for (hipEvent_t e : {s->evc_ready, s->evc_halo, s->evc_band, s->evc_int})
-    if (e) (void)hipEventDestroy(e);
-  if (s->ev_fork) (void)hipEventDestroy(s->ev_fork);
-  if (s->ev_join) (void)hipEventDestroy(s->ev_join);
-  if (s->ev_join2) (void)hipEventDestroy(s->ev_join2);
   if (s->comm && !keep_comm) ncclCommDestroy(s->comm);
   (void)hipFree(s->snap_dev);
   if (s->snap_host) (void)hipHostFree(s->snap_host);
@@ -1856,76 +1837,37 @@ int fold_events(nlh_solver *s, bool drain) {
 
 // ---- HIP graphs of production passes (NLH_GRAPH=1)
 // A run of g passes is captured once per (g, start parity) and replayed with
-// one hipGraphLaunch on s_main: the pass launches, and with an exchange every
-// pass's interior / bands / pack / unpack / local block copies on the streams
-// and with the cross-stream order of the ungraphed schedule (the side
-// streams fork from s_main at the start and join it at the end).  The
-// kernels and their arguments are the ungraphed ones: bitwise equal fields.
-// Production mode only (test mode's per-step source constants are kernel
-// arguments), kernel timing 0 / 1 only, once the halo is fresh -- and only
-// for solvers without RCCL messages: with grouped ncclSend / ncclRecv inside
-// the capture the process died in nlh_run (SIGSEGV) in 2 of 3 whole-suite
-// runs on MI355X (RCCL 2.27.7, send/recv to self; the same test alone, and
-// the suite under pytest -s, passed), and on ROCm 7.2 a graph launch costs
-// the host about what its nodes' direct launches cost with an exchange
-// (per pass 86 -> 73 us for C3's 8 virtual ranks, profiles/r06/graph), so
-// graphs stay an option, off by default.
+// one hipGraphLaunch on s_main.  The kernels and their arguments are the
+// ungraphed ones: bitwise equal fields.  Production mode only (test mode's
+// per-step source constants are kernel arguments), kernel timing 0 / 1 only,
+// and only for single-stream solvers (no exchange).  Measured on MI355X with
+// ROCm 7.2 (profiles/r06/graph): a graph launch costs
+// the host about what its nodes' direct launches cost once side streams are
+// in it (C3's 8 virtual ranks: 86 -> 73 us of enqueue per pass), and graphs
+// with the exchange on side streams -- captured with fork / join events, with
+// or without grouped ncclSend / ncclRecv inside -- killed the process with
+// SIGSEGV inside nlh_run in 3 of 4 whole-suite runs (never alone, never
+// under pytest -s); on one stream (one block) it halves nlh_run's enqueue
+// (32 -> 13-18 us for 10 passes) and changes nothing the GPU sees.  So the
+// exchange passes stay ungraphed and graphs stay an option, off by default.
 constexpr int kGraphMaxPasses = 16;
 
 int graph_passes(const nlh_solver *s, int64_t passes_left) {
   if (!s->graph_on || s->p.test || (s->timing != 0 && s->timing != 1)) return 0;
-  if (s->exchange && (!s->halo_fresh || s->passes_enqueued < 2 || !s->peers.empty())) return 0;
+  if (s->exchange) return 0;
   int g = 0;
   for (int c = 2; c <= kGraphMaxPasses && c <= passes_left; c *= 2) g = c;
   return g;
 }
 
 int capture_graph(nlh_solver *s, int g, int spp, hipGraphExec_t *out) {
-  if (s->exchange && !s->ev_fork) {
-    for (hipEvent_t *e : {&s->ev_fork, &s->ev_join, &s->ev_join2, &s->evc_ready, &s->evc_halo, &s->evc_band,
-                          &s->evc_int})
-      HIP_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming));
-  }
-  // the capture records and waits on its own events, never on the ones the
-  // ungraphed schedule records outside it
-  auto swap_events = [s] {
-    std::swap(s->ev_ready, s->evc_ready);
-    std::swap(s->ev_halo, s->evc_halo);
-    std::swap(s->ev_band, s->evc_band);
-    std::swap(s->ev_int, s->evc_int);
-  };
   const int64_t t0 = s->t, steps0 = s->timed_steps, passes0 = s->timed_passes;
   const int cur0 = s->cur;
-  const bool band_stream = s->exchange && s->sched == 0;
   HIP_TRY(hipStreamBeginCapture(s->s_main, hipStreamCaptureModeRelaxed));
-  if (s->exchange) swap_events();
   int rc = NLH_OK;
-  auto body = [&]() -> int {
-    if (s->exchange) {
-      HIP_TRY(hipEventRecord(s->ev_fork, s->s_main));
-      HIP_TRY(hipStreamWaitEvent(s->s_comm, s->ev_fork, 0));
-      if (band_stream) HIP_TRY(hipStreamWaitEvent(s->s_band, s->ev_fork, 0));
-    }
-    for (int j = 0; j < g; ++j) {
-      s->capture_first = j == 0;
-      const int r = enqueue_step(s, spp);
-      s->capture_first = false;
-      if (r) return r;
-    }
-    if (s->exchange) {
-      HIP_TRY(hipEventRecord(s->ev_join, s->s_comm));
-      HIP_TRY(hipStreamWaitEvent(s->s_main, s->ev_join, 0));
-      if (band_stream) {
-        HIP_TRY(hipEventRecord(s->ev_join2, s->s_band));
-        HIP_TRY(hipStreamWaitEvent(s->s_main, s->ev_join2, 0));
-      }
-    }
-    return NLH_OK;
-  };
-  rc = body();
+  for (int j = 0; j < g && rc == NLH_OK; ++j) rc = enqueue_step(s, spp);
   hipGraph_t graph = nullptr;
   const hipError_t ec = hipStreamEndCapture(s->s_main, &graph);
-  if (s->exchange) swap_events();
   s->t = t0;
   s->cur = cur0;
   s->timed_steps = steps0;
@@ -1941,9 +1883,7 @@ int capture_graph(nlh_solver *s, int g, int spp, hipGraphExec_t *out) {
   return NLH_OK;
 }
 
-// g passes from the current step: the captured graph (captured now if new),
-// ordered after everything enqueued before on every stream, and every later
-// cross-stream wait ordered after it
+// g passes from the current step: the captured graph (captured now if new)
 int launch_graph(nlh_solver *s, int g, int spp) {
   nlh_solver::Graph *ge = nullptr;
   for (auto &x : s->graphs)
@@ -1956,16 +1896,7 @@ int launch_graph(nlh_solver *s, int g, int spp) {
     s->graphs.push_back(n);
     ge = &s->graphs.back();
   }
-  if (s->exchange) {
-    HIP_TRY(hipStreamWaitEvent(s->s_main, s->ev_halo, 0));  // bands(n-1) and the exchange for halo(n)
-    if (s->sched == 0) HIP_TRY(hipStreamWaitEvent(s->s_main, s->ev_band, 0));
-  }
   HIP_TRY(hipGraphLaunch(ge->exec, s->s_main));
-  if (s->exchange) {
-    HIP_TRY(hipEventRecord(s->ev_int, s->s_main));
-    HIP_TRY(hipEventRecord(s->ev_band, s->s_main));
-    HIP_TRY(hipEventRecord(s->ev_halo, s->s_main));
-  }
   if (g & 1) s->cur = 1 - s->cur;
   s->t += (int64_t)g * spp;
   if (s->timing) {
@@ -2281,7 +2212,6 @@ int nlh_run(nlh_solver *s, int64_t nsteps) {
       continue;
     }
     if ((rc = enqueue_step(s, spp)) || (rc = fold()) || (rc = probe())) return rc;
-    ++s->passes_enqueued;
     i += spp;
   }
   for (; i < nsteps; ++i)

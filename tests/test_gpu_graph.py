@@ -1,16 +1,12 @@
 """GPU: production passes replayed from captured HIP graphs (NLH_GRAPH=1,
 VERDICT r5 next 4) give the ungraphed path's field bit for bit.
 
-The graphs hold the same kernels with the same arguments and, with an
-exchange, the same cross-stream order (interior on the main stream, bands +
-pack + unpack + local block copies on the exchange stream), so every layout
-must match the ungraphed run exactly: one block, blocks exchanging by device
-copies under each band schedule, the single-step kernels, call sequences that
-mix graph runs with ungraphed remainders and odd step counts, and kernel
-timing around graph launches.  Solvers with RCCL messages (blocks over RCCL
-to self, virtual ranks) keep their passes ungraphed (nlh_api.cpp
-graph_passes: RCCL inside a capture crashed intermittently) and must still
-match.
+Graphs hold the same kernels with the same arguments.  A single-stream
+solver (one block) replays runs of 2..16 passes per hipGraphLaunch; solvers
+with an exchange keep their passes ungraphed (nlh_api.cpp graph_passes:
+multi-stream captures crashed intermittently on ROCm 7.2, DESIGN.md section
+6) and must match too.  Call sequences mix graph runs with ungraphed
+remainders and odd step counts; kernel timing brackets graph launches.
 """
 import numpy as np
 import pytest
