@@ -320,7 +320,8 @@ typedef struct {
   const nlh_oracle_params *p;
   const double *u;
   double *un;
-  const long double *pu, *pw; /* row prefix sums, (nx + 1) per row */
+  const long double *pu;      /* row prefix sums of u, (nx + 1) per row */
+  const long double *lw;      /* test mode: sum_disk W0~_j - N W0_i per node (W0 = sx sy), fixed */
   const long *len;            /* len(|d|), d = 0 .. eps */
   const double *sx_tab, *sy_tab;
   long double cdh2, st, ct;
@@ -341,19 +342,18 @@ static void *comp_rows(void *arg) {
   const long double dt = (long double)j->p->dt;
   for (long y = j->y0; y < j->y1; ++y)
     for (long x = 0; x < nx; ++x) {
-      long double su = 0.0L, sw = 0.0L;
+      long double su = 0.0L;
       for (long dy = -eps; dy <= eps; ++dy) {
         const long yy = y + dy;
         if (yy < 0 || yy >= ny) continue;
-        const long L = j->len[labs(dy)];
-        su += window_sum(j->pu + yy * (nx + 1), nx, x, L);
-        if (j->p->test) sw += window_sum(j->pw + yy * (nx + 1), nx, x, L);
+        su += window_sum(j->pu + yy * (nx + 1), nx, x, j->len[labs(dy)]);
       }
       const long double ui = (long double)j->u[x + y * nx];
       long double r = j->cdh2 * (su - N * ui);
       if (j->p->test) {
+        /* w~ = ct W0~: its disk sum is ct times W0's, computed once */
         const long double w0 = (long double)j->sx_tab[x + eps] * (long double)j->sy_tab[y + eps];
-        r += -(2.0L * (long double)M_PI * j->st) * w0 - j->cdh2 * (sw - N * (j->ct * w0));
+        r += -(2.0L * (long double)M_PI * j->st) * w0 - j->cdh2 * (j->ct * j->lw[x + y * nx]);
       }
       j->un[x + y * nx] = (double)(ui + dt * r);
     }
@@ -365,11 +365,30 @@ void nlh_oracle_run_compensated(const nlh_oracle_params *p, long nt, double *u, 
   const size_t n = (size_t)(nx * ny);
   double *b = (double *)malloc(sizeof(double) * (n ? n : 1));
   long double *pu = (long double *)malloc(sizeof(long double) * (size_t)(ny * (nx + 1)));
-  long double *pw = p->test ? (long double *)malloc(sizeof(long double) * (size_t)(ny * (nx + 1))) : NULL;
+  long double *lw = p->test ? (long double *)malloc(sizeof(long double) * (n ? n : 1)) : NULL;
   long *len = (long *)malloc(sizeof(long) * (size_t)(eps + 1));
   for (long d = 0; d <= eps; ++d) len[d] = line_len(eps, d);
   step_ctx c;
   ctx_init(&c, p);
+  if (lw) {
+    /* sum_disk W0~_j - N W0_i once, from row windows of W0's prefix sums */
+    const long double N = (long double)nlh_oracle_disk_count(eps);
+    for (long y = 0; y < ny; ++y) {
+      long double *r = pu + y * (nx + 1);
+      r[0] = 0.0L;
+      for (long x = 0; x < nx; ++x)
+        r[x + 1] = r[x] + (long double)c.sx_tab[x + eps] * (long double)c.sy_tab[y + eps];
+    }
+    for (long y = 0; y < ny; ++y)
+      for (long x = 0; x < nx; ++x) {
+        long double sw = 0.0L;
+        for (long dy = -eps; dy <= eps; ++dy) {
+          const long yy = y + dy;
+          if (yy >= 0 && yy < ny) sw += window_sum(pu + yy * (nx + 1), nx, x, len[labs(dy)]);
+        }
+        lw[x + y * nx] = sw - N * ((long double)c.sx_tab[x + eps] * (long double)c.sy_tab[y + eps]);
+      }
+  }
   if (nthreads < 1) nthreads = 1;
   if (nthreads > ny) nthreads = ny > 0 ? (int)ny : 1;
   pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)nthreads);
@@ -379,14 +398,8 @@ void nlh_oracle_run_compensated(const nlh_oracle_params *p, long nt, double *u, 
     ctx_time(&c, t);
     for (long y = 0; y < ny; ++y) {
       long double *r = pu + y * (nx + 1);
-      long double *q = pw ? pw + y * (nx + 1) : NULL;
       r[0] = 0.0L;
-      if (q) q[0] = 0.0L;
-      for (long x = 0; x < nx; ++x) {
-        r[x + 1] = r[x] + (long double)cur[x + y * nx];
-        if (q)
-          q[x + 1] = q[x] + (long double)c.ct * (long double)c.sx_tab[x + eps] * (long double)c.sy_tab[y + eps];
-      }
+      for (long x = 0; x < nx; ++x) r[x + 1] = r[x] + (long double)cur[x + y * nx];
     }
     for (int i = 0; i < nthreads; ++i) {
       comp_job *j = &jobs[i];
@@ -394,7 +407,7 @@ void nlh_oracle_run_compensated(const nlh_oracle_params *p, long nt, double *u, 
       j->u = cur;
       j->un = nxt;
       j->pu = pu;
-      j->pw = pw;
+      j->lw = lw;
       j->len = len;
       j->sx_tab = c.sx_tab;
       j->sy_tab = c.sy_tab;
@@ -419,7 +432,7 @@ void nlh_oracle_run_compensated(const nlh_oracle_params *p, long nt, double *u, 
   free(jobs);
   free(th);
   free(len);
-  free(pw);
+  free(lw);
   free(pu);
   free(b);
 }

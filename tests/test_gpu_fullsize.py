@@ -94,3 +94,50 @@ def test_c2_full_run_length_test_mode():
     assert info.steps_per_pass == 2 and info_e.kernel == N.KERNEL_EXACT
     check_nodes(uf, ue, "C2 1000 steps test mode: k_pair_split<TEST> vs k_exact")
     check_l2(l2f, l2e, uf, ue, "C2 1000 steps test mode: k_pair_split<TEST> vs k_exact")
+
+
+NT_COMP = 100
+
+
+@pytest.mark.parametrize("test", [False, True])
+def test_c2_vs_compensated_oracle(oracle, test):
+    """C2's lattice against the compensated oracle (the same steps in long
+    double, one rounding per node and step; round 6): the two-step kernel
+    within 1e-12 of field scale per node and, in test mode, its L2 by the
+    criterion of conftest.check_l2 against the compensated L2.  The
+    bit-parity kernel (the reference's own order) is measured against the
+    same target and recorded: at C2 the reference's L2 sits at its field's
+    rounding floor, which this separates from the fast
+    kernel's error.  100 steps: the oracle takes ~30 s on the box's host share."""
+    import json
+    import os
+
+    from conftest import _record_dir, node_errors
+    dh = 1.0 / NX
+    dt = EPS ** 4 * dh * dh / (8 * N.disk_count(EPS))
+    p = oracle.params(NX, NX, EPS, 1.0, dt, dh, int(test))
+    u0 = oracle.test_init(p)
+    ref = oracle.run_compensated(p, NT_COMP, u0)
+    l2_ref = oracle.errors(p, NT_COMP, ref)[0]
+    out = {}
+    for kernel in ("fast", "exact"):
+        with N.Solver(NX, NX, EPS, 1.0, dt, dh, test=test, kernel=kernel) as s:
+            s.input_init(u0)
+            s.run(NT_COMP)
+            s.synchronize()
+            out[kernel] = (s.field(), s.errors(NT_COMP)[0], s.info())
+    uf, l2f, info = out["fast"]
+    assert info.steps_per_pass == 2 and info.pass_kernel == "k_pair_split"
+    mode = "test mode" if test else "production"
+    check_nodes(uf, ref, f"C2 {NT_COMP} steps {mode}: k_pair_split vs the compensated oracle")
+    ue, l2e, _ = out["exact"]
+    st = node_errors(ue, ref)
+    rec = {"test": os.environ.get("PYTEST_CURRENT_TEST", "").split(" ")[0],
+           "what": f"C2 {NT_COMP} steps {mode}: k_exact (the reference's order) vs the compensated oracle (recorded)",
+           "n": int(ref.size), **st}
+    if test:
+        check_l2(l2f, l2_ref, uf, ref, f"C2 {NT_COMP} steps test mode: k_pair_split vs the compensated oracle")
+        rec.update(l2=l2e, l2_compensated=l2_ref, l2_fast=l2f, l2_rel_diff_reference_order=abs(l2e - l2_ref) / l2_ref,
+                   l2_rel_diff_fast=abs(l2f - l2_ref) / l2_ref)
+    with open(os.path.join(_record_dir(), "parity_nodes.jsonl"), "a") as f:
+        f.write(json.dumps(rec) + "\n")
