@@ -2109,8 +2109,12 @@ int nlh_barrier(nlh_solver *s) {
   if (!s) return fail(NLH_ERR_ARG, "null solver");
   int rc = set_device(s);
   if (rc) return rc;
-  HIP_TRY(hipStreamSynchronize(s->s_main));
-  HIP_TRY(hipStreamSynchronize(s->s_comm));
+  if (s->sync_mode != 0) {
+    HIP_TRY(hipStreamSynchronize(s->s_main));
+    HIP_TRY(hipStreamSynchronize(s->s_comm));
+  } else if ((rc = poll_stream(s, s->s_main, false)) || (rc = poll_stream(s, s->s_comm, false))) {
+    return rc;
+  }
   if (s->comm) {
     NCCL_TRY(ncclAllReduce(s->d_red, s->d_red, 1, ncclDouble, ncclSum, s->comm, s->s_comm));
     HIP_TRY(hipStreamSynchronize(s->s_comm));
@@ -2170,8 +2174,9 @@ int nlh_snapshot_wait(nlh_solver *s, double *u) {
 int nlh_run(nlh_solver *s, int64_t nsteps) {
   if (!s) return fail(NLH_ERR_ARG, "null solver");
   if (nsteps < 0) return fail(NLH_ERR_ARG, "negative step count");
-  s->h_enter = now_ns();
+  s->h_enter = s->h_return = now_ns();  // h_return moves on only when the run was enqueued
   s->h_start_seen = s->h_end_seen = -1;
+  s->h_sync_return = 0;
   s->h_e0 = s->h_e1 = nullptr;
   int rc = set_device(s);
   if (rc) return rc;
