@@ -86,8 +86,8 @@ enum nlh_influence { NLH_INFLUENCE_CONSTANT = 0, NLH_INFLUENCE_LINEAR = 1 };
  * error is itself at that floor (l2 ~ 1e-20 .. 1e-11: few steps, large
  * eps) the L2 difference is bounded by B instead.
  * AUTO = FAST (production and test mode) except where FAST cannot apply,
- * which runs EXACT: k*dt*dh = 0 past eps 16; eps > 992 (the chunked
- * run-time kernel's LDS prefix row); J = 1 - r past eps 52 (the weighted
+ * which runs EXACT: k*dt*dh = 0 past eps 16; eps > 4832 (the chunked
+ * run-time kernel's two LDS prefix rows fill 160 KB); J = 1 - r past eps 52 (the weighted
  * tile past 160 KB of LDS).  An explicit FAST request there is refused.  */
 enum nlh_kernel { NLH_KERNEL_AUTO = 0, NLH_KERNEL_EXACT = 1, NLH_KERNEL_FAST = 2 };
 

@@ -4,7 +4,8 @@
 namespace nlh {
 
 // 65 .. 224: one staged chunk (k_prefix_rt); past 224 the chunked k_prefix_rtc
-// up to kPrefixMaxE (its LDS: 2 (64 x 8 x nchk + 2) doubles <= 41 KB)
+// up to kPrefixMaxE (its LDS: 2 (64 x 8 x nchk + 2) doubles, nchk <= 19:
+// <= 152 KB, one workgroup per CU at the largest horizons)
 bool prefix_rt_supported(int E) { return E >= 65 && E <= kPrefixMaxE; }
 
 // chunks of 64 x 8 columns k_prefix_rtc stages (64 + 2E rounded up to even)
@@ -47,6 +48,7 @@ int launch_prefix_rt(const RectList &rl, const StepConst &c, const void *table, 
   if (c.E <= 224) return test ? launch_nv<8, true>(rl, c, table, st) : launch_nv<8, false>(rl, c, table, st);
   if (c.E > kPrefixMaxE) return -1;
   const int nchk = prefix_rtc_chunks(c.E);
+  if (nchk > kPrefixMaxChunks) return -1;
   const size_t lds = 2 * (size_t)(512 * nchk + 2) * sizeof(double);
   if (test)
     hipLaunchKernelGGL((k_prefix_rtc<8, kPrefixRows, true>), dim3(rl.nwork), dim3(64), lds, st, rl, c,

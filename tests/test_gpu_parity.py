@@ -295,10 +295,11 @@ def test_prefix_rtc_blocks(oracle, monkeypatch):
     check_nodes(u, ref, "k_prefix_rtc eps 231, 3x2 blocks")
 
 
-@pytest.mark.parametrize("eps", [993, 1100])
+@pytest.mark.parametrize("eps", [4833, 5000])
 def test_unsupported_fast_eps_falls_back_to_exact(oracle, eps):
-    """Past k_prefix_rtc's range (eps > 992: its LDS) AUTO runs the exact
-    kernel and an explicit FAST request is refused."""
+    """Past k_prefix_rtc's range (eps > 4832: its two prefix slots of 19
+    chunks fill the CU's 160 KB of LDS) AUTO runs the exact kernel and an
+    explicit FAST request is refused."""
     r = N.BatchRow(60, 50, 2, eps, 1.0, 1e-4, 1.0 / 60)
     with N.Solver(r.nx, r.ny, eps, r.k, r.dt, r.dh, test=False, kernel="auto") as s:
         assert s.info().kernel == N.KERNEL_EXACT
