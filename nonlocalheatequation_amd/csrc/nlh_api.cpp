@@ -181,6 +181,8 @@ constexpr EnvKnob kEnvKnobs[] = {
     {"NLH_SEGV_TRACE", 0, 1},      // diagnostics: a native backtrace on stderr on SIGSEGV / SIGBUS
     {"NLH_PAIR_PRIO", 0, 2},       // k_pair_split wave priority: 0 never, 1 one-round lists (default), 2 not on bands
     {"NLH_TRACE_REPART", 0, 1},    // repartition phase times on stderr
+    {"NLH_PREFIX_ROWS", 0, 128},   // k_prefix_rt / k_prefix_rtc output rows per work item (32, 64; 96, 128 past
+                                   // eps 224; 0: by eps)
 };
 constexpr const char *kRemovedKnobs[] = {"NLH_ABLATE", "NLH_PAIR_ABLATE"};
 
@@ -306,6 +308,7 @@ struct nlh_solver {
   bool weighted = false;  // k_weighted: non-constant influence function
   bool prefix = false;    // k_prefix_rt (nlh_prefix.h) past the k_wide horizons
   int32_t *d_ptab = nullptr;  // k_prefix_rt's per-offset prefix index table
+  int prefix_rows = 0;        // its R (output rows per work item: nlh::prefix_rt_rows)
   double *d_lsx = nullptr, *d_lty = nullptr;  // fast test mode, J = 1: separable L_h[W0] tables (sep_tables)
   int sep_nlv = 0, sep_lts = 0;                // their level count and lty row stride
   double *d_wt = nullptr, *d_qj = nullptr;  // J tables (influence != 0)
@@ -522,7 +525,7 @@ int build_rectlists(nlh_solver *s, int kind) {
         }
         seg_h = own ? s->p.seg_rows : (int)best;
       } else if (s->prefix) {
-        seg_h = nlh::kPrefixRows;  // the kernel's register block of output rows
+        seg_h = s->prefix_rows;  // the kernel's register block of output rows
       } else if (s->wide) {
         // k_wide: one-wave workgroups, all resident in one round: two waves per
         // SIMD up to E = 40 (8 per CU, 214 VGPRs at E = 32;
@@ -1254,6 +1257,11 @@ int create_impl(const nlh_params *pin, nlh_solver *s, ncclComm_t reuse_comm = nu
   s->wide = rv.wide;
   s->weighted = rv.weighted;
   s->prefix = rv.prefix;
+  if (s->prefix) {
+    s->prefix_rows = nlh::prefix_rt_rows(E);
+    if (!nlh::prefix_rt_rows_ok(E, s->prefix_rows))
+      return fail(NLH_ERR_ARG, "NLH_PREFIX_ROWS must be 32 or 64 (96 or 128 past eps 224)");
+  }
   if (const char *fb = std::getenv("NLH_FORCE_BANDS")) s->force_bands = std::atoi(fb) != 0;
   if (const char *rs = std::getenv("NLH_RCCL_SELF")) s->rccl_self = p.nranks == 1 && std::atoi(rs) != 0;
   if (vranks) s->rccl_self = true;  // virtual owners talk over RCCL to self
@@ -1345,8 +1353,8 @@ int create_impl(const nlh_params *pin, nlh_solver *s, ncclComm_t reuse_comm = nu
   s->sc.nf = (double)s->disk;
   s->sc.kc = (s->pair || s->wide || s->prefix) ? 1.0 / s->sc.alpha - s->sc.nf : 0.0;
   if (s->prefix) {
-    std::vector<int32_t> tab(2 * (size_t)nlh::prefix_rt_table_size(E));
-    nlh::prefix_rt_table(E, lens.data(), tab.data());
+    std::vector<int32_t> tab(2 * (size_t)nlh::prefix_rt_table_size(E, s->prefix_rows));
+    nlh::prefix_rt_table(E, s->prefix_rows, lens.data(), tab.data());
     HIP_TRY(hipMalloc(&s->d_ptab, tab.size() * sizeof(int32_t)));
     HIP_TRY(hipMemcpy(s->d_ptab, tab.data(), tab.size() * sizeof(int32_t), hipMemcpyHostToDevice));
   }

@@ -8,6 +8,14 @@
 namespace nlh {
 
 constexpr int kPrefixRows = 32;  // R: output rows per work item (the rect lists' seg_rows)
+// taller register blocks (R = 64 .. 128): the scan of each staged row is
+// shared by more output rows -- for the chunked kernel, whose scan of 64 + 2E
+// columns outweighs a row's R pairs at large eps.  R a solver's prefix kernels
+// use at horizon E (NLH_PREFIX_ROWS overrides; 0 or unset: by E); the launch
+// takes it from the rect list's seg_rows, the table from the solver.
+// k_prefix_rt: R = 32, 64; k_prefix_rtc (E > 224): 32, 64, 96, 128
+int prefix_rt_rows(int E);
+bool prefix_rt_rows_ok(int E, int R);
 // horizons k_prefix_rt serves: 65 .. 224 (staged window 64 + 2E <= 512
 // columns), k_prefix_rtc past that (the window in 512-column chunks).  Its
 // two prefix slots of 512 nchk + 2 doubles fit a CU's 160 KB of LDS up to
@@ -21,10 +29,10 @@ bool prefix_rt_supported(int E);
 int prefix_rt_window(int E);
 // host table of 2 (E + R) + 1 int2 entries, index d + E + R: {L, -L - 1}
 // with L = len(|d|) for |d| <= E, {0, 0} beyond
-int prefix_rt_table_size(int E);
+int prefix_rt_table_size(int E, int R);
 // output columns per work item (64 x the kernel's columns per lane)
 int prefix_rt_strip_width(int E);
-void prefix_rt_table(int E, const int32_t *lens, int32_t *out);
+void prefix_rt_table(int E, int R, const int32_t *lens, int32_t *out);
 int launch_prefix_rt(const RectList &rl, const StepConst &c, const void *table, bool test, void *stream);
 
 // rows a pair-pass solver allocates beyond each block's halo rows, above and
