@@ -181,6 +181,7 @@ constexpr EnvKnob kEnvKnobs[] = {
     {"NLH_SEGV_TRACE", 0, 1},      // diagnostics: a native backtrace on stderr on SIGSEGV / SIGBUS
     {"NLH_PAIR_PRIO", 0, 2},       // k_pair_split wave priority: 0 never, 1 one-round lists (default), 2 not on bands
     {"NLH_TRACE_REPART", 0, 1},    // repartition phase times on stderr
+    {"NLH_PREFIX_WAVES", 0, 16},   // prefix kernels: waves per workgroup sharing a staged row (1, 2, 4, 8, 16; 0: by eps)
     {"NLH_PREFIX_ROWS", 0, 128},   // k_prefix_rt / k_prefix_rtc output rows per work item (32, 64; 96, 128 past
                                    // eps 224; 0: by eps)
 };
@@ -309,6 +310,7 @@ struct nlh_solver {
   bool prefix = false;    // k_prefix_rt (nlh_prefix.h) past the k_wide horizons
   int32_t *d_ptab = nullptr;  // k_prefix_rt's per-offset prefix index table
   int prefix_rows = 0;        // its R (output rows per work item: nlh::prefix_rt_rows)
+  int prefix_waves = 1;       // waves per workgroup sharing a staged row (nlh::prefix_rt_waves)
   double *d_lsx = nullptr, *d_lty = nullptr;  // fast test mode, J = 1: separable L_h[W0] tables (sep_tables)
   int sep_nlv = 0, sep_lts = 0;                // their level count and lty row stride
   double *d_wt = nullptr, *d_qj = nullptr;  // J tables (influence != 0)
@@ -465,7 +467,7 @@ int build_rectlists(nlh_solver *s, int kind) {
   const bool pair = kind == 1;
   const int sw = pair        ? nlh::pair_strip_width(E)
                  : !fast     ? 64
-                 : s->prefix ? nlh::prefix_rt_strip_width(E)
+                 : s->prefix ? nlh::prefix_rt_strip_width(E, s->prefix_waves)
                              : nlh::fast_strip_width(E, s->fast_r);
   // gather local rects (bands are s->halo wide: what the halo exchange refreshes)
   struct Item { int blk; LRect r; };
@@ -771,7 +773,7 @@ int launch_stencil(nlh_solver *s, RLIter b, RLIter e, hipStream_t st) {
     if (s->weighted)
       rc = nlh::launch_weighted(rl, s->sc, test, st);
     else if (s->prefix)
-      rc = nlh::launch_prefix_rt(rl, s->sc, s->d_ptab, test, st);
+      rc = nlh::launch_prefix_rt(rl, s->sc, s->d_ptab, test, s->prefix_waves, st);
     else if (s->wide)
       rc = nlh::launch_wide(rl, s->sc, test, st);
     else if (s->kernel == NLH_KERNEL_FAST)
@@ -1258,7 +1260,10 @@ int create_impl(const nlh_params *pin, nlh_solver *s, ncclComm_t reuse_comm = nu
   s->weighted = rv.weighted;
   s->prefix = rv.prefix;
   if (s->prefix) {
-    s->prefix_rows = nlh::prefix_rt_rows(E);
+    s->prefix_waves = nlh::prefix_rt_waves(E);
+    if (!nlh::prefix_rt_waves_ok(E, s->prefix_waves))
+      return fail(NLH_ERR_ARG, "NLH_PREFIX_WAVES must be 1, 2, 4, 8 or 16 (its window within the LDS)");
+    s->prefix_rows = nlh::prefix_rt_rows(E, s->prefix_waves);
     if (!nlh::prefix_rt_rows_ok(E, s->prefix_rows))
       return fail(NLH_ERR_ARG, "NLH_PREFIX_ROWS must be 32 or 64 (96 or 128 past eps 224)");
   }
@@ -1388,7 +1393,7 @@ int create_impl(const nlh_params *pin, nlh_solver *s, ncclComm_t reuse_comm = nu
     // (k_prefix_rt stages 64 NV <= 512 columns from x0 - E of its last strip,
     // k_prefix_rtc 512-column chunks: prefix_rt_window)
     const int64_t right = std::max({round_up(b.r.w, 256) + XL, s->pair ? b.r.w + 128 : (int64_t)0,
-                                    s->prefix ? round_up(b.r.w, 64) + nlh::prefix_rt_window(E) : (int64_t)0});
+                                    s->prefix ? round_up(b.r.w, 64) + nlh::prefix_rt_window(E, s->prefix_waves) : (int64_t)0});
     b.pitch = round_up(XL + right, 8) + pitch_pad;
     // pair passes: padding rows beyond the halo rows, above and below, that
     // k_pair_split's tail row DMAs read instead of clamping (nlh_pair.h)

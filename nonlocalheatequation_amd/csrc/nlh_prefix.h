@@ -323,4 +323,126 @@ __global__ __launch_bounds__(64) void k_prefix_rtc(RectList L, StepConst C, cons
   }
 }
 
+// k_prefix_rtw: k_prefix_rtc with W waves per workgroup sharing one staged
+// prefix row (round 6).  The workgroup owns 64 W adjacent output columns x R
+// rows; its window 64 W + 2E is staged in nchk chunks of 512 columns, chunk k
+// scanned by wave k mod W, so each wave scans ~nchk / W chunks per row instead
+// of the whole 64 + 2E window of its own 64 columns.  Per row:
+//   scan:  each wave's chunks -> local prefix (no carry) into slot s, chunk
+//          totals into tot[s];                                   s_barrier
+//   carry: each wave adds the sum of the earlier chunks' totals to its
+//          chunks' values (read-modify-write of its own LDS);    s_barrier
+//   pairs: each wave's 64 columns, k_prefix_rt's pair loop on slot s.
+// Slot s alternates per row, so the next row's scan (slot s ^ 1) never waits
+// for the other waves' pair loops: two barriers per row.  Same prefix
+// values as k_prefix_rtc up to the order of the carry additions (the carry
+// is the sum of chunk totals, then added to the chunk's local prefix).
+template <int NV, int R, bool TEST, int W>
+__global__ __launch_bounds__(64 * W) void k_prefix_rtw(RectList L, StepConst C, const int2 *__restrict__ tab,
+                                                       int nchk) {
+  extern __shared__ __attribute__((aligned(16))) double pfd[];
+  constexpr int CW = 64 * NV;          // columns per chunk
+  const int npf = CW * nchk + 2;       // doubles per slot: [0] = P(-1) = 0, [1 + k] = P(k)
+  double *tot = pfd + 2 * npf;         // [2][nchk] chunk totals
+  const int lane = (int)threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  const int E = C.E;
+  const int work = xcd_remap(blockIdx.x, gridDim.x);
+  const int ri = find_rect(L, work);
+  const Rect &Rc = L.r[ri];
+  const int local = work - Rc.wg_begin;
+  const int strip = local % Rc.nstrip, seg = local / Rc.nstrip;
+  const int x0 = Rc.x0 + strip * (64 * W);
+  const int y0 = Rc.y0 + seg * Rc.seg_rows;
+  const int nout = min(R, Rc.y1 - y0);
+  const int64_t pitch = Rc.pitch;
+  const int xl = x0 + 64 * wv + lane;
+  if (threadIdx.x == 0) {
+    pfd[0] = 0.0;
+    pfd[npf] = 0.0;
+  }
+  const int EP = E + (E & 1);
+  const double *gcol = Rc.u + (x0 - EP + NV * lane);
+  auto load_chunk = [&](int r, int c, double (&v)[NV]) __attribute__((always_inline)) {
+    const double2 *g = reinterpret_cast<const double2 *>(gcol + (int64_t)r * pitch + CW * c);
+#pragma unroll
+    for (int k = 0; k < NV / 2; ++k) {
+      const double2 w = g[k];
+      v[2 * k] = w.x;
+      v[2 * k + 1] = w.y;
+    }
+  };
+  double acc[R];
+#pragma unroll
+  for (int j = 0; j < R; ++j) acc[j] = 0.0;
+
+  const int rfirst = y0 - E, rend = y0 + nout + E;
+  // this wave's chunks: wv, wv + W, ..; the first one's values prefetched
+  double cur[NV], nxt[NV];
+  if (wv < nchk) load_chunk(rfirst, wv, cur);
+  for (int r = rfirst; r < rend; ++r) {
+    const int s = (r - rfirst) & 1;
+    double *slot = pfd + s * npf;
+    double *ts = tot + s * nchk;
+    for (int c = wv; c < nchk; c += W) {
+      // the wave's next chunk of this row, or its first chunk of the next row
+      if (c + W < nchk)
+        load_chunk(r, c + W, nxt);
+      else if (r + 1 < rend)
+        load_chunk(r + 1, wv, nxt);
+      double p[NV];
+      p[0] = cur[0];
+#pragma unroll
+      for (int k = 1; k < NV; ++k) p[k] = p[k - 1] + cur[k];
+      const double incl = rt_wave_prefix(p[NV - 1]);
+      const double ex = incl - p[NV - 1];
+      double *dst = slot + 1 + CW * c + NV * lane;
+#pragma unroll
+      for (int k = 0; k < NV; ++k) dst[k] = ex + p[k];
+      if (lane == 63) ts[c] = incl;
+#pragma unroll
+      for (int k = 0; k < NV; ++k) cur[k] = nxt[k];
+    }
+    __syncthreads();
+    // carry: chunk c's values += total of chunks 0 .. c-1 (lane k holds the
+    // inclusive sum of totals 0 .. k after a wave scan; nchk <= 64)
+    {
+      const double tk = lane < nchk ? ts[lane] : 0.0;
+      const double ik = rt_wave_prefix(tk);
+      for (int c = wv + (wv == 0 ? W : 0); c < nchk; c += W) {
+        const double carry = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(ik), c - 1),
+                                              __builtin_amdgcn_readlane(__double2loint(ik), c - 1));
+        double *dst = slot + 1 + CW * c + NV * lane;
+#pragma unroll
+        for (int k = 0; k < NV; ++k) dst[k] += carry;
+      }
+    }
+    __syncthreads();
+    const int2 *t = tab + (r - y0 + E + R);
+    const double *cen = slot + 1 + EP + 64 * wv + lane;  // the lane's P(c), c = EP + 64 wv + lane
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const int2 o = t[-j];  // {L, -L - 1}, or {0, 0} past the horizon
+      acc[j] += cen[o.x] - cen[o.y];
+    }
+  }
+  const double alpha = C.alpha, kc = C.kc;
+  const double qs = TEST ? C.dt / alpha : 0.0;
+  const bool emit = xl < Rc.x1;
+  const double sxv = TEST ? C.sxt[Rc.gx0 + min(xl, Rc.x1 - 1) + E] : 0.0;
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+    if (j < nout && emit) {
+      const int64_t off = (int64_t)(y0 + j) * pitch + xl;
+      double a = fma(kc, Rc.u[off], acc[j]);
+      if constexpr (TEST) {
+        const double syv = C.syt[Rc.gy0 + y0 + j + E];
+        const double b = -(C.st2pi * (sxv * syv)) - C.ct * Rc.lw[off];
+        a = fma(qs, b, a);
+      }
+      Rc.un[off] = alpha * a;
+    }
+  }
+}
+
 }  // namespace nlh

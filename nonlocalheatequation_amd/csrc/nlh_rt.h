@@ -9,12 +9,13 @@ namespace nlh {
 
 constexpr int kPrefixRows = 32;  // R: output rows per work item (the rect lists' seg_rows)
 // taller register blocks (R = 64 .. 128): the scan of each staged row is
-// shared by more output rows -- for the chunked kernel, whose scan of 64 + 2E
-// columns outweighs a row's R pairs at large eps.  R a solver's prefix kernels
-// use at horizon E (NLH_PREFIX_ROWS overrides; 0 or unset: by E); the launch
-// takes it from the rect list's seg_rows, the table from the solver.
-// k_prefix_rt: R = 32, 64; k_prefix_rtc (E > 224): 32, 64, 96, 128
-int prefix_rt_rows(int E);
+// shared by more output rows -- for the single-wave chunked kernel, whose
+// scan of 64 + 2E columns outweighs a row's R pairs at large eps.  R a
+// solver's prefix kernels use at horizon E with W waves per workgroup
+// (NLH_PREFIX_ROWS overrides; 0 or unset: by E and W); the launch takes it
+// from the rect list's seg_rows, the table from the solver.
+// k_prefix_rt: R = 32, 64; k_prefix_rtc / k_prefix_rtw (E > 224): 32, 64, 96, 128
+int prefix_rt_rows(int E, int W);
 bool prefix_rt_rows_ok(int E, int R);
 // horizons k_prefix_rt serves: 65 .. 224 (staged window 64 + 2E <= 512
 // columns), k_prefix_rtc past that (the window in 512-column chunks).  Its
@@ -25,15 +26,20 @@ constexpr int kPrefixMaxChunks = 19;
 constexpr int kPrefixMaxE = (512 * kPrefixMaxChunks - 64) / 2;  // 4832 (even: no +2)
 static_assert(2 * (512 * kPrefixMaxChunks + 2) * 8 <= 160 * 1024, "k_prefix_rtc slots exceed the LDS");
 bool prefix_rt_supported(int E);
+// waves per workgroup of the prefix kernels (W > 1: k_prefix_rtw, W waves
+// sharing one staged prefix row; NLH_PREFIX_WAVES = 1, 2, 4, 8, 16
+// overrides); the solver fixes W, then R, at nlh_create
+int prefix_rt_waves(int E);
+bool prefix_rt_waves_ok(int E, int W);
 // columns staged from x0 - E of a strip (the block's right padding covers them)
-int prefix_rt_window(int E);
+int prefix_rt_window(int E, int W);
 // host table of 2 (E + R) + 1 int2 entries, index d + E + R: {L, -L - 1}
 // with L = len(|d|) for |d| <= E, {0, 0} beyond
 int prefix_rt_table_size(int E, int R);
 // output columns per work item (64 x the kernel's columns per lane)
-int prefix_rt_strip_width(int E);
+int prefix_rt_strip_width(int E, int W);
 void prefix_rt_table(int E, int R, const int32_t *lens, int32_t *out);
-int launch_prefix_rt(const RectList &rl, const StepConst &c, const void *table, bool test, void *stream);
+int launch_prefix_rt(const RectList &rl, const StepConst &c, const void *table, bool test, int waves, void *stream);
 
 // rows a pair-pass solver allocates beyond each block's halo rows, above and
 // below (nlh_pair.h kPairPadRows: k_pair_split's tail row DMAs read them)

@@ -83,6 +83,41 @@ def test_prefix_rtc_huge_eps_stable_dt(oracle, eps, nx, ny, test):
     _case(oracle, eps, test, nx, ny, 2, "k_prefix_rt")
 
 
+PREFIX_FORMS = [(w, r) for w in (1, 2, 4, 8, 16) for r in (32, 64, 96, 128)]
+
+
+@pytest.mark.parametrize("eps", [200, 301])
+@pytest.mark.parametrize("waves,rows", PREFIX_FORMS, ids=[f"W{w}-R{r}" for w, r in PREFIX_FORMS])
+def test_prefix_forms_stable_dt(oracle, monkeypatch, eps, waves, rows):
+    """Round 6: every launched prefix form -- k_prefix_rt / k_prefix_rtc (W =
+    1) and k_prefix_rtw (W waves sharing one staged prefix row, 2 .. 16) at R
+    = 32 .. 128 output rows per work item (NLH_PREFIX_WAVES / NLH_PREFIX_ROWS;
+    the library picks W and R by eps) -- against the compensated oracle at the
+    stable dt, production mode; odd eps 301 (8-byte-aligned window loads).
+    Forms the library refuses (R = 96 / 128 at eps <= 224) raise."""
+    monkeypatch.setenv("NLH_PREFIX_WAVES", str(waves))
+    monkeypatch.setenv("NLH_PREFIX_ROWS", str(rows))
+    if eps <= 224 and rows > 64:
+        with pytest.raises(N.NLHError, match="NLH_PREFIX_ROWS"):
+            N.Solver(300, 280, eps, 1.0, 1e-9, 1.0 / 300, kernel="fast")
+        return
+    _case(oracle, eps, False, 2 * eps + 157, 2 * eps + 71, 2, "k_prefix_rt", seed=3)
+
+
+def test_prefix_wave_limits():
+    """W > 1 needs its window 64 W + 2 eps in the LDS's 19 chunks: W = 16 up
+    to eps 4352, W = 1 to 4832; past that the knob is refused."""
+    for eps, ok in ((4352, True), (4353, False)):
+        with pytest.MonkeyPatch.context() as mp:
+            mp.setenv("NLH_PREFIX_WAVES", "16")
+            if ok:
+                with N.Solver(64, 48, eps, 1.0, 1e-9, 1.0 / 64, kernel="fast") as s:
+                    assert s.info().pass_kernel == "k_prefix_rt"
+            else:
+                with pytest.raises(N.NLHError, match="NLH_PREFIX_WAVES"):
+                    N.Solver(64, 48, eps, 1.0, 1e-9, 1.0 / 64, kernel="fast")
+
+
 @pytest.mark.parametrize("eps", [1200, 4832])
 def test_huge_eps_fast_vs_exact(eps):
     """The fast kernel against k_exact (bitwise the reference order,
