@@ -202,8 +202,9 @@ typedef struct nlh_info {
   int32_t steps_per_pass;  /* 2: production fast mode fuses two steps per
                               pass over HBM (one halo exchange per pass)   */
   char    pass_kernel[32]; /* device kernel of one full pass: "k_pair_split",
-                              "k_fast", "k_wide", "k_weighted", "k_exact_lds"
-                              or "k_exact"                                 */
+                              "k_fast", "k_wide", "k_prefix_rt",
+                              "k_prefix_rtw", "k_prefix_rtc", "k_weighted",
+                              "k_exact_lds" or "k_exact"                   */
   int32_t owners;          /* owner ids in the tile map: nranks, or the
                               NLH_VIRTUAL_RANKS count (nlh_rebalance sizes) */
   int32_t comm_nranks;     /* ranks of the RCCL communicator as RCCL reports

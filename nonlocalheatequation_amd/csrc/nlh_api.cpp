@@ -2345,7 +2345,9 @@ int nlh_get_info(const nlh_solver *s, nlh_info *info) {
   info->comm_nranks = s->comm_nranks;
   info->comm_rank = s->comm_rank;
   const char *pk = s->pair ? "k_pair_split"
-                           : s->wide ? "k_wide" : s->prefix ? "k_prefix_rt" : s->weighted ? "k_weighted"
+                           : s->wide ? "k_wide"
+                           : s->prefix ? (s->prefix_waves > 1 ? "k_prefix_rtw" : s->p.eps > 224 ? "k_prefix_rtc" : "k_prefix_rt")
+                           : s->weighted ? "k_weighted"
                            : s->kernel == NLH_KERNEL_FAST ? "k_fast"
                            : nlh::exact_lds_ok((int)s->p.eps, s->p.test != 0) ? "k_exact_lds" : "k_exact";
   std::snprintf(info->pass_kernel, sizeof(info->pass_kernel), "%s", pk);

@@ -45,7 +45,7 @@ def _case(oracle, eps, test, nx, ny, nt, kernel_name, tiles=(1, 1), seed=0):
         u = s.field()
         info = s.info()
         l2 = s.errors(nt)[0] if test else None
-    assert info.pass_kernel == kernel_name and info.kernel == N.KERNEL_FAST, info
+    assert info.pass_kernel.startswith(kernel_name) and info.kernel == N.KERNEL_FAST, info
     scale = max(float(np.max(np.abs(u0))), float(np.max(np.abs(ref))))
     check_nodes(u, ref, f"{kernel_name} eps {eps} stable dt vs compensated oracle", scale=scale)
     if test:
@@ -112,7 +112,7 @@ def test_prefix_wave_limits():
             mp.setenv("NLH_PREFIX_WAVES", "16")
             if ok:
                 with N.Solver(64, 48, eps, 1.0, 1e-9, 1.0 / 64, kernel="fast") as s:
-                    assert s.info().pass_kernel == "k_prefix_rt"
+                    assert s.info().pass_kernel.startswith("k_prefix_rt")
             else:
                 with pytest.raises(N.NLHError, match="NLH_PREFIX_WAVES"):
                     N.Solver(64, 48, eps, 1.0, 1e-9, 1.0 / 64, kernel="fast")
@@ -139,7 +139,7 @@ def test_huge_eps_fast_vs_exact(eps):
             s.synchronize()
             out[kern] = s.field()
             if kern == "fast":
-                assert s.info().pass_kernel == "k_prefix_rt"
+                assert s.info().pass_kernel.startswith("k_prefix_rt")
     check_nodes(out["fast"], out["exact"], f"k_prefix_rtc eps {eps} vs k_exact")
 
 
