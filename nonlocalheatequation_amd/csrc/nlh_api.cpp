@@ -162,7 +162,7 @@ struct EnvKnob {
 constexpr EnvKnob kEnvKnobs[] = {
     {"NLH_PAIR", 0, 1},            // 0: single-step kernels instead of the two-step pass
     {"NLH_FAST_R", 1, 4},          // k_fast columns per lane (1, 2 or 4)
-    {"NLH_FORCE_BANDS", 0, 1},     // exchange-path schedule on a single block
+    {"NLH_FORCE_BANDS", 0, 31},    // exchange-path schedule on a single block: 1 all sides, or 2 L | 4 R | 8 T | 16 B
     {"NLH_RCCL_SELF", 0, 1},       // one rank: halo pieces over RCCL to self
     {"NLH_VIRTUAL_RANKS", 0, 1024},  // run V virtual ranks in this process
     {"NLH_INT_PER_CU", 0, 64},     // interior workgroups per CU beside an exchange
@@ -328,7 +328,9 @@ struct nlh_solver {
   hipStream_t s_main = nullptr, s_comm = nullptr, s_band = nullptr;
   hipEvent_t ev_ready = nullptr, ev_halo = nullptr, ev_band = nullptr, ev_int = nullptr;
   bool halo_fresh = false;  // the current field's halo holds its neighbours' values
-  bool force_bands = false;  // diagnostics (NLH_FORCE_BANDS): exchange-path schedule on one block
+  // diagnostics (NLH_FORCE_BANDS): exchange-path schedule on one block, bands
+  // on the sides of the mask (1: all four; else 2 left, 4 right, 8 top, 16 bottom)
+  int force_bands = 0;
   bool rccl_self = false;    // diagnostics (NLH_RCCL_SELF): one rank, local pieces over RCCL to self
   bool exchange_planned = false;  // the plan has halo pieces (set before the rect lists)
   int vranks = 0;       // NLH_VIRTUAL_RANKS count (0: one real rank per process)
@@ -719,7 +721,7 @@ int build_exchange(nlh_solver *s) {
       if (rc != NLH_OK) return rc;
     }
   }
-  s->exchange = !s->plan.pieces.empty() || s->force_bands;
+  s->exchange = !s->plan.pieces.empty() || s->force_bands != 0;
   return NLH_OK;
 }
 
@@ -1267,7 +1269,7 @@ int create_impl(const nlh_params *pin, nlh_solver *s, ncclComm_t reuse_comm = nu
     if (!nlh::prefix_rt_rows_ok(E, s->prefix_rows))
       return fail(NLH_ERR_ARG, "NLH_PREFIX_ROWS must be 32 or 64 (96 or 128 past eps 224)");
   }
-  if (const char *fb = std::getenv("NLH_FORCE_BANDS")) s->force_bands = std::atoi(fb) != 0;
+  if (const char *fb = std::getenv("NLH_FORCE_BANDS")) s->force_bands = std::atoi(fb) == 1 ? 30 : std::atoi(fb) & 30;
   if (const char *rs = std::getenv("NLH_RCCL_SELF")) s->rccl_self = p.nranks == 1 && std::atoi(rs) != 0;
   if (vranks) s->rccl_self = true;  // virtual owners talk over RCCL to self
   if (const char *ic = std::getenv("NLH_INT_PER_CU")) s->int_per_cu = std::max(0, std::atoi(ic));
@@ -1398,10 +1400,10 @@ int create_impl(const nlh_params *pin, nlh_solver *s, ncclComm_t reuse_comm = nu
     // pair passes: padding rows beyond the halo rows, above and below, that
     // k_pair_split's tail row DMAs read instead of clamping (nlh_pair.h)
     b.rows = b.r.h + 2 * (s->halo + (s->pair ? nlh::pair_pad_rows() : 0));
-    b.L = b.r.x0 > 0 || s->force_bands;
-    b.Rr = b.r.x0 + b.r.w < p.nx || s->force_bands;
-    b.T = b.r.y0 > 0 || s->force_bands;
-    b.B = b.r.y0 + b.r.h < p.ny || s->force_bands;
+    b.L = b.r.x0 > 0 || (s->force_bands & 2);
+    b.Rr = b.r.x0 + b.r.w < p.nx || (s->force_bands & 4);
+    b.T = b.r.y0 > 0 || (s->force_bands & 8);
+    b.B = b.r.y0 + b.r.h < p.ny || (s->force_bands & 16);
     const size_t bytes = (size_t)(b.pitch * b.rows) * sizeof(double);
     // zeroed on s_main (a non-blocking stream: a null-stream hipMemset is not
     // ordered before work on it), and waited for below, before anything --
@@ -1421,7 +1423,7 @@ int create_impl(const nlh_params *pin, nlh_solver *s, ncclComm_t reuse_comm = nu
   HIP_TRY(hipStreamSynchronize(s->s_main));
   trace_mark("c_blocks");
 
-  s->exchange_planned = !s->plan.pieces.empty() || s->force_bands;
+  s->exchange_planned = !s->plan.pieces.empty() || s->force_bands != 0;
   int rc = build_rectlists(s, 0);
   if (rc) return rc;
   if (s->pair && (rc = build_rectlists(s, 1))) return rc;
