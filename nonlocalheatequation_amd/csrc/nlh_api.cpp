@@ -545,12 +545,16 @@ int build_rectlists(nlh_solver *s, int kind) {
     // halo bands run beside the interior kernel (enqueue_step); their segments
     // are short -- about one band workgroup per CU -- so that bands, the
     // exchange they feed and the next pass's bands fit inside one interior
-    // pass.  NLH_BAND_SEG overrides the height (diagnostics)
+    // pass, but (two-step pass) not below 4E rows: a three-sided 4096^2 rank (left strip +
+    // top / bottom bands: 21-row segments) ran 89-97 us per pass against
+    // 80-83 with 32-64-row band segments, one side or four 78-85 either way
+    // (round 6, profiles/r06/rank_proxy/seg/).  NLH_BAND_SEG overrides the
+    // height (diagnostics)
     int seg_band = seg_h;
     if (fast) {
       int64_t band_rows = 0;
       for (auto &it : bnd) band_rows += ceil_div(it.r.x1 - it.r.x0, sw) * (it.r.y1 - it.r.y0);
-      const int lo = std::min(seg_h, 2 * E);
+      const int lo = std::min(seg_h, (pair ? 4 : 2) * E);
       seg_band = (int)std::min<int64_t>(seg_h, std::max<int64_t>(lo, ceil_div(band_rows, (int64_t)s->cus)));
       if (const char *bsg = std::getenv("NLH_BAND_SEG"))
         if (std::atoi(bsg) > 0) seg_band = std::atoi(bsg);
