@@ -338,16 +338,24 @@ struct nlh_solver {
   int owners = 1;  // owner ids in the tile map: nranks, or NLH_VIRTUAL_RANKS
   // exchange schedule: interior workgroups per CU in the segment model when
   // an exchange runs beside it (NLH_INT_PER_CU, 0 = all the pass kernel's
-  // slots), and where the bands run (NLH_SCHED): 2 = on the exchange stream
-  // (default), 0 = own stream beside the interior, 1 = before the interior on
-  // s_main.  Round 4: all slots (0) beat round 1's 3 per CU on one rank's
+  // slots), and where the bands run (NLH_SCHED): 0 = own stream beside the
+  // interior (default since round 6), 2 = on the exchange stream (rounds
+  // 1-5), 1 = before the interior on s_main.  Round 6, one rank's pass with
+  // the exchange-path schedule forced on its sides (tools/rank_proxy.py,
+  // profiles/r06/rank_proxy/sched/): a C3 rank (16384 x 8192, 2-3 sides)
+  // 502-505 us per pass with 0 against 600-611 with 2 (518 alone), a 9216^2
+  // C5 tile with 3 sides 357-360 against 405-413, 4096^2 ranks with 1-3 sides
+  // 78.5-79.3 against 79.8-81.1; only a four-sided 4096^2 block ran worse
+  // (84.9 / 91.6 against 80.8-82.6), a layout the 2x1 / 2x2 / 2x4 runs do not
+  // have; the virtual-rank lines (C3, C5, weak 2 / 4 / 8) within +-1% except
+  // C3's, +3.4%.  Round 4: all slots (0) beat round 1's 3 per CU on one rank's
   // blocks over RCCL to self -- 4096^2 as 2x1 blocks 82 vs 88-90 us per pass,
   // 8192x4096 as 2x1 156-157 vs 164-166, 8192^2 as 2x2 290-295 vs 296-298
   // (profiles/r04/sched); the pass kernel's 4 workgroups per CU hold 252 of
   // 512 VGPRs per SIMD lane and 56 of 160 KB of LDS, so bands and RCCL
   // kernels still find room beside them
   int int_per_cu = 0;
-  int sched = 2;
+  int sched = 0;
   int64_t t = 0;
   int cur = 0;
   double *d_sxt = nullptr, *d_syt = nullptr;

@@ -603,7 +603,7 @@ def test_linear_influence_large_eps_uses_exact():
 # FAST within 1e-12 of field scale)
 ENV_KNOBS = [("NLH_PAIR", "0"), ("NLH_FAST_R", "1"), ("NLH_FAST_R", "4"), ("NLH_FORCE_BANDS", "1"),
              ("NLH_FORCE_BANDS", "26"),
-             ("NLH_RCCL_SELF", "1"), ("NLH_VIRTUAL_RANKS", "3"), ("NLH_INT_PER_CU", "1"), ("NLH_SCHED", "0"),
+             ("NLH_RCCL_SELF", "1"), ("NLH_VIRTUAL_RANKS", "3"), ("NLH_INT_PER_CU", "1"), ("NLH_SCHED", "2"),
              ("NLH_SCHED", "1"), ("NLH_COMM_PRIO", "1"), ("NLH_PAIR_SPLIT", "4"), ("NLH_PAIR_CU", "2"),
              ("NLH_PAIR_TEST", "0"), ("NLH_PITCH_PAD", "6"), ("NLH_BAND_SEG", "5")]
 
