@@ -1,3 +1,8 @@
+#!/bin/bash
+# Round 6 trial (a library build with the NLH_XQ knob under the bands-own-
+# stream schedule, removed again after this run): memory-value waits vs event
+# waits on the 4096^2 rank proxies, with a kernel trace.  Result: worse
+# (profiles/r06/rank_proxy/timeline/).
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/r6xq2; mkdir -p $O
