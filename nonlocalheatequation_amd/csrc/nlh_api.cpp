@@ -1313,8 +1313,14 @@ int create_impl(const nlh_params *pin, nlh_solver *s, ncclComm_t reuse_comm = nu
     HIP_TRY(hipStreamCreateWithPriority(&s->s_band, hipStreamNonBlocking, prio_hi));
     HIP_TRY(hipEventCreateWithFlags(&s->ev_ready, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&s->ev_halo, hipEventDisableTiming));
-    HIP_TRY(hipEventCreateWithFlags(&s->ev_band, hipEventDisableTiming));
-    HIP_TRY(hipEventCreateWithFlags(&s->ev_int, hipEventDisableTiming));
+    // the per-pass kernel -> kernel dependencies between the interior and the
+    // band streams (one device, device memory only): device-scope release /
+    // acquire instead of the system-scope fence.  Round 6, 4096^2 rank proxy
+    // (tools/gpu/r6_evfence.sh, profiles/r06/rank_proxy/evfence/): one side
+    // 76.4-76.8 against 78.0-79.2 us per pass, three sides 76.2-76.5 against
+    // 78.8-79.3 (the main queue's gap at these two events)
+    HIP_TRY(hipEventCreateWithFlags(&s->ev_band, hipEventDisableTiming | hipEventDisableSystemFence));
+    HIP_TRY(hipEventCreateWithFlags(&s->ev_int, hipEventDisableTiming | hipEventDisableSystemFence));
   }
   HIP_TRY(hipEventRecord(s->ev_band, s->s_main));
   HIP_TRY(hipEventRecord(s->ev_int, s->s_main));
